@@ -1,0 +1,223 @@
+"""Capture golden vectors from the reference renderer (run in the survey container).
+
+Imports the reference's own ``Renderer`` / ``Network`` from ``/root/reference``
+(read-only), with empty stand-ins for the two I/O-only imports it does not use
+on this path (``imageio``, ``cv2``: ``volume_renderer.py:4,7``), loads the
+deterministic synthetic weights from ``nerfhip.synthetic`` and renders small
+crops of the lego test camera on the CPU. Every ``torch.rand`` draw the
+reference makes during ``render`` is recorded so tests can replay it.
+
+Outputs ``tests/golden/<name>.npz`` (inputs + the 8 output maps + a few
+intermediates). Nothing from the reference's source is stored — only the
+numbers it produced.
+
+    python tests/golden/make_golden.py            # all fixtures
+    python tests/golden/make_golden.py f1 f3      # selected
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+
+sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
+from nerfhip.synthetic import make_params, params_digest, make_occupancy_grid, load_into_network  # noqa: E402
+
+LEGO_TEST_FRAME0 = None  # filled from the dataset json
+
+
+def _import_reference():
+    sys.argv = ["make_golden", "--cfg_file", "configs/nerf/lego.yaml"]
+    os.chdir(REF)
+    sys.path.insert(0, REF)
+    for m in ("imageio", "cv2"):
+        sys.modules.setdefault(m, types.ModuleType(m))
+    import torch  # noqa: F401
+    from src.config import cfg
+    from src.models.nerf.network import Network
+    import src.models.nerf.renderer.volume_renderer as vr
+    return cfg, Network, vr
+
+
+# name: (H, W, full_res, crop x0, y0, frame, weights(seed, gain, alpha_bias), cfg overrides, extra)
+FIXTURES = {
+    # F1: lego 800^2 test frame 0, centre crop, 64c+128f, ESS/ERT off, perturb 0, eval
+    "f1_c2_crop": dict(H=32, W=32, res=800, x0=384, y0=384, frame=0, w=(0, 2.0, 0.0),
+                       cfg=dict(N_importance=128, perturb=0, enable_ess=False, enable_ert=False)),
+    # F2: F1 with stratified jitter (captured t_rand)
+    "f2_c2_perturb": dict(H=32, W=32, res=800, x0=384, y0=384, frame=0, w=(0, 2.0, 0.0),
+                          cfg=dict(N_importance=128, perturb=1, enable_ess=False, enable_ert=False)),
+    # F2b: dense weights, off-centre crop, frame 7 (different rotation)
+    "f2b_c2_dense": dict(H=24, W=40, res=800, x0=300, y0=420, frame=7, w=(1, 3.0, 1.0),
+                         cfg=dict(N_importance=128, perturb=0, enable_ess=False, enable_ert=False)),
+    # F3: ERT on, 2 chunks (2048 + 256 rays), mixed termination -> argmax quirk
+    "f3_ert": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                   cfg=dict(N_importance=128, perturb=0, enable_ess=False, enable_ert=True,
+                            ert_threshold=0.01)),
+    # F3b: ERT on but no ray in the chunk reaches the threshold (weights untouched)
+    "f3b_ert_noterm": dict(H=16, W=16, res=800, x0=392, y0=392, frame=0, w=(1, 3.0, 1.0),
+                           cfg=dict(N_importance=128, perturb=0, enable_ess=False, enable_ert=True,
+                                    ert_threshold=0.01)),
+    # F4: ESS + ERT, deterministic grid, update frozen (grid_update_counter=1)
+    "f4_ess_ert": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                       cfg=dict(N_importance=128, perturb=0, enable_ess=True, enable_ert=True,
+                                ert_threshold=0.01),
+                       grid=dict(seed=3, radius=0.55, noise=0.02), counter=1),
+    # F4b: ESS + ERT with the call-0 grid self-update (counter 0), perturb on
+    "f4b_ess_ert_update": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                               cfg=dict(N_importance=128, perturb=1, enable_ess=True,
+                                        enable_ert=True, ert_threshold=0.01),
+                               grid=dict(seed=4, radius=0.5, noise=0.01), counter=0),
+    # F5: lego 400^2 camera crop, 64 coarse only
+    "f5_c1_crop": dict(H=32, W=32, res=400, x0=184, y0=184, frame=0, w=(0, 2.0, 0.0),
+                       cfg=dict(N_importance=0, perturb=0, enable_ess=False, enable_ert=False)),
+    # F6: ragged 1x7 strip, lindisp
+    "f6_ragged_lindisp": dict(H=1, W=7, res=800, x0=396, y0=400, frame=3, w=(2, 2.0, 0.5),
+                              cfg=dict(N_importance=128, perturb=0, enable_ess=False,
+                                       enable_ert=False, lindisp=True)),
+}
+
+
+def _camera(spec, frames, angle):
+    res = spec["res"]
+    focal = 0.5 * res / np.tan(0.5 * angle)            # blender.py:41-42
+    pose = np.array(frames[spec["frame"]]["transform_matrix"], np.float32)
+    K = np.array([[focal, 0, res / 2 - spec["x0"]],
+                  [0, focal, res / 2 - spec["y0"]],
+                  [0, 0, 1]], np.float32)
+    return pose, K
+
+
+def capture(name, spec, cfg, Network, vr, frames, angle):
+    import torch
+    for k in ("N_importance", "perturb", "lindisp"):
+        if k in spec["cfg"]:
+            cfg.task_arg[k] = spec["cfg"][k]
+    cfg.task_arg.lindisp = spec["cfg"].get("lindisp", False)
+    for k in ("enable_ess", "enable_ert", "ert_threshold"):
+        if k in spec["cfg"]:
+            cfg[k] = spec["cfg"][k]
+    seed, gain, ab = spec["w"]
+    params = make_params(seed, gain, ab)
+    net = Network()
+    load_into_network(net, params)
+    net.eval()
+    torch.manual_seed(1234)
+    rend = vr.Renderer(net)
+    rend.use_cuda_kernels = False
+    grid = None
+    if "grid" in spec:
+        g = spec["grid"]
+        grid = make_occupancy_grid(g["seed"], 128, g["radius"], g["noise"])
+        rend.occupancy_grid = torch.from_numpy(grid.copy())
+        rend.grid_update_counter = spec.get("counter", 0)
+    pose, K = _camera(spec, frames, angle)
+
+    draws = []
+    orig_rand = torch.rand
+
+    def rec_rand(*a, **kw):
+        t = orig_rand(*a, **kw)
+        draws.append(t.detach().clone().numpy())
+        return t
+
+    inter = {}
+    NSTAGE = 256   # rays whose per-stage intermediates are stored (first chunk)
+    orig_q = rend._query_network
+    comp_name = "_raw2outputs_with_ert" if rend.enable_ert else "_raw2outputs"
+    orig_c = getattr(rend, comp_name)
+    calls = {"n": 0}
+
+    def chunk_any(raw, z, rays_d):
+        # the chunk-wide `low_transmittance.any()` decision (volume_renderer.py:1108-1116)
+        d = torch.cat([z[..., 1:] - z[..., :-1], torch.full_like(z[..., :1], 1e10)], -1)
+        d = d * torch.norm(rays_d[..., None, :], dim=-1)
+        a = 1. - torch.exp(-torch.relu(raw[..., 3]) * d)
+        sh = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+        return bool((torch.cumprod(1.0 - sh, 1) < rend.ert_threshold).any())
+
+    def rec_c(raw, z, rays_d):
+        r = orig_c(raw, z, rays_d)
+        if rend.enable_ert and calls["n"] < 2:
+            inter["chunk_any_%d" % calls["n"]] = np.array(chunk_any(raw, z, rays_d))
+        if calls["n"] == 0:                      # coarse pass of chunk 0
+            inter["zc"] = z[:NSTAGE].detach().numpy().copy()
+            inter["wc"] = r[3][:NSTAGE].detach().numpy().copy()
+        elif calls["n"] == 1 and rend.N_importance > 0:   # fine pass of chunk 0
+            inter["zall"] = z[:NSTAGE].detach().numpy().copy()
+        calls["n"] += 1
+        return r
+
+    setattr(rend, comp_name, rec_c)
+
+    def rec_q(pts, vd, model):
+        raw = orig_q(pts, vd, model)
+        key = "coarse" if model is rend.coarse_model else "fine"
+        if key + "_pts" not in inter:
+            inter[key + "_pts"] = pts[:16].detach().numpy().copy()
+            inter[key + "_raw"] = raw[:16].detach().numpy().copy()
+        return raw
+
+    rend._query_network = rec_q
+    batch = {"H": spec["H"], "W": spec["W"], "pose": torch.from_numpy(pose)[None],
+             "intrinsics": torch.from_numpy(K)[None]}
+    torch.rand = rec_rand
+    try:
+        with torch.no_grad():
+            out = rend.render(batch)
+    finally:
+        torch.rand = orig_rand
+    n = spec["H"] * spec["W"]
+    rec = dict(
+        H=spec["H"], W=spec["W"], pose=pose, K=K,
+        w_seed=seed, w_gain=gain, w_alpha_bias=ab, w_digest=params_digest(params),
+        N_samples=cfg.task_arg.N_samples, N_importance=cfg.task_arg.N_importance,
+        perturb=float(cfg.task_arg.perturb), lindisp=bool(cfg.task_arg.lindisp),
+        enable_ess=bool(rend.enable_ess), enable_ert=bool(rend.enable_ert),
+        ert_threshold=float(rend.ert_threshold), near=float(rend.near), far=float(rend.far),
+        white_bkgd=bool(rend.white_bkgd), grid_counter_in=spec.get("counter", 0),
+        grid_counter_out=rend.grid_update_counter,
+    )
+    if "grid" in spec:
+        rec.update(grid_seed=spec["grid"]["seed"], grid_radius=spec["grid"]["radius"],
+                   grid_noise=spec["grid"]["noise"],
+                   grid_out_packed=np.packbits(rend.occupancy_grid.numpy().reshape(-1)))
+    if rec["perturb"] > 0:
+        # one [chunk, N_samples] draw per 2048-ray chunk (volume_renderer.py:233, :1083)
+        coarse = [d for d in draws if d.ndim == 2 and d.shape[1] == rec["N_samples"]]
+        rec["t_rand"] = np.concatenate(coarse, 0)[:n]
+    for k, v in out.items():
+        rec["out_" + k] = v.numpy()
+    for k, v in inter.items():
+        rec["int_" + k] = v
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(f"{name}: {spec['H']}x{spec['W']} -> {os.path.getsize(path) / 1024:.1f} KiB, "
+          f"keys={sorted(out.keys())}")
+
+
+def main(argv):
+    cfg, Network, vr = _import_reference()
+    meta = json.load(open(os.path.join(REF, "data/nerf_synthetic/lego/transforms_test.json")))
+    frames, angle = meta["frames"], meta["camera_angle_x"]
+    names = argv or list(FIXTURES)
+    for name in names:
+        key = [k for k in FIXTURES if k == name or k.startswith(name + "_")]
+        if not key:
+            raise SystemExit(f"unknown fixture {name}")
+        capture(key[0], FIXTURES[key[0]], cfg, Network, vr, frames, angle)
+    # the lego test poses travel with the repo (bench/tests on the GPU box)
+    poses = np.array([f["transform_matrix"] for f in frames], np.float32)
+    np.savez_compressed(os.path.join(OUT, "lego_test_cameras.npz"), poses=poses,
+                        camera_angle_x=np.float64(angle))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
