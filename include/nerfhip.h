@@ -1,0 +1,219 @@
+/*
+ * nerfhip.h — C ABI of the MI355X (gfx950) NeRF volume-render library.
+ *
+ * Plain pointers and sizes only; every device pointer is HBM memory on the
+ * current HIP device; every call takes an explicit stream (hipStream_t passed
+ * as void*) and is asynchronous on it. Return value: 0 on success, otherwise
+ * an error code (NERF_E_*) or a hipError_t; nerf_last_error() then holds a
+ * message for the calling thread. Nothing here calls exit().
+ *
+ * Two groups of entry points:
+ *   1. the render path of the reference PyTorch renderer
+ *      (src/models/nerf/renderer/volume_renderer.py, "VR" below), split into
+ *      the stages the reference runs per 2048-ray chunk;
+ *   2. the op contract of the reference extension module `kilonerf_cuda`
+ *      (cuda/pybind.cu:11-39), one kn_* function per op, same argument meaning.
+ * Reference citations are file:line in the reference repository.
+ */
+#ifndef NERFHIP_H
+#define NERFHIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* nerf_stream_t; /* hipStream_t */
+
+enum {
+  NERF_OK = 0,
+  NERF_E_ARG = 1001,      /* bad argument (null pointer, size out of range) */
+  NERF_E_UNSUPPORTED = 1002,
+  NERF_E_LAUNCH = 1003,   /* kernel launch failed */
+  NERF_E_HANDLE = 1004    /* unknown grouped-GEMM handle */
+};
+
+const char* nerf_last_error(void);
+int nerf_version(void);                 /* ABI version, bumped on layout changes */
+
+/* ---------------------------------------------------------------------------
+ * 1. Render path
+ * ------------------------------------------------------------------------- */
+
+/* Packed MLP layout: one 8x256 NeRF MLP = NERF_MLP_SLICES
+ * slices of 32 KiB (MFMA A-fragments in consumption order) + a head block of
+ * NERF_MLP_HEAD_FLOATS floats (lane-packed biases, density and rgb heads). */
+#define NERF_MLP_SLICES 73
+#define NERF_MLP_SLICE_FLOATS 8192
+#define NERF_MLP_HEAD_FLOATS 3200
+
+/* VR:115-143: camera rays for pixels [p0, p0+n) of an H x W image (row-major,
+ * pixel p -> (y = p / W, x = p % W), integer pixel centres), origin = pose
+ * translation, unit-length direction R·((x-cx)/fx, -(y-cy)/fy, -1) / |·|.
+ * cam (device) = pose[16] (4x4 row-major) followed by K[9] (3x3 row-major).
+ * rays_o, rays_d: [n][3] float32. */
+int nerf_rays(const float* cam, int H, int W, int64_t p0, int64_t n,
+              float* rays_o, float* rays_d, nerf_stream_t stream);
+
+/* VR:218-237: coarse depths z[n][S]. z_base (device, [S]) is the reference's
+ * torch.linspace-derived depth table; t_rand (device, [n][S], or NULL for
+ * perturb = 0) the stratification draws. */
+int nerf_sample_coarse(const float* z_base, const float* t_rand, int64_t n, int S,
+                       float* z, nerf_stream_t stream);
+
+/* NET:49-74 on samples pts = o + d*z of n rays x S samples (VR:165, VR:270-284):
+ * frequency encoding (L=10 xyz, L=4 dir) fused with the 8x256 MLP, FP32 MFMA.
+ * z row stride z_stride floats (0 = one shared row). raw: [n*S][4] = (rgb
+ * logits, sigma raw). w_slices/w_head: packed by nerfhip.pack (device). */
+int nerf_mlp_forward(const float* w_slices, const float* w_head,
+                     const float* rays_o, const float* rays_d,
+                     const float* z, int64_t z_stride, int64_t n, int S,
+                     float* raw, nerf_stream_t stream);
+
+/* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
+ * Reductions follow torch's CPU float32 summation order.
+ * Outputs rgb[n][3], disp/acc/depth[n]; weights[n][S] optional (NULL). */
+int nerf_composite(const float* raw, const float* z, int64_t z_stride,
+                   const float* rays_d, int64_t n, int S, int white_bkgd,
+                   float* rgb, float* disp, float* acc, float* depth, float* weights,
+                   nerf_stream_t stream);
+
+/* VR:1089-1133: compositing with early ray termination, including the
+ * chunk-wide argmax behaviour: rays are grouped in chunks of `chunk` rays
+ * (2048 in the reference, VR:147) counted from ray 0 of this call. */
+int nerf_composite_ert(const float* raw, const float* z, int64_t z_stride,
+                       const float* rays_d, int64_t n, int S, int white_bkgd,
+                       float threshold, int chunk,
+                       float* rgb, float* disp, float* acc, float* depth, float* weights,
+                       nerf_stream_t stream);
+
+/* VR:239-268 + VR:181-183: inverse-CDF fine sampling from the coarse weights
+ * and merge: z_all[n][S+n_imp] = sort(concat(z, samples)).
+ * u: [n_imp] (u_stride 0, eval) or [n][n_imp] (training draws). */
+int nerf_sample_fine(const float* z, int64_t z_stride, const float* weights,
+                     const float* u, int64_t u_stride, int64_t n, int S, int n_imp,
+                     float* z_all, nerf_stream_t stream);
+
+/* VR:1009-1087 empty-space skipping for whole chunks of `chunk` rays: per
+ * chunk one shared depth row folded over its "highly empty" rays in ray order
+ * (the reference's expand()-shared row), then optional stratification.
+ * grid: bool[res^3] (x-major, [x][y][z]) over the box [-2,2]^3. S <= 64. */
+int nerf_sample_coarse_ess(const float* rays_o, const float* rays_d,
+                           const uint8_t* grid, int res, const float* z_base,
+                           const float* t_rand, int64_t n, int S, int chunk,
+                           float skip_threshold, float* z, nerf_stream_t stream);
+
+/* VR:1147-1155 / VR:963-990: occupancy-grid self-update: cells of points
+ * d*z (no origin, as the reference) with weight > 1e-4 and relu(sigma) > 0.01
+ * are set. */
+int nerf_grid_update(const float* rays_d, const float* z, int64_t z_stride,
+                     const float* raw, const float* weights, int64_t n, int S,
+                     uint8_t* grid, int res, nerf_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * 2. kilonerf_cuda op contract (cuda/pybind.cu:13-38)
+ * ------------------------------------------------------------------------- */
+
+/* cuda/generate_inputs.cu:11-52 — un-normalised R·((x-cx)/fx, -(y-cy)/fy, -1),
+ * out [H][W][3]; c2w (device) 3x3 row-major. */
+int kn_get_rays_d(int H, int W, float cx, float cy, float fx, float fy,
+                  const float* c2w, float* out, nerf_stream_t stream);
+
+/* cuda/generate_inputs.cu:60-192 */
+int kn_generate_query_indices_on_ray(const float* origin, const float* directions, int num_rays,
+                                     const int16_t* occupancy_grid, uint8_t* active_ray_mask,
+                                     int16_t* depth_indices, const float* voxel_size,
+                                     const float* global_domain_min, const float* global_domain_max,
+                                     const int32_t* strides, float distance_between_points,
+                                     int max_samples_per_ray, int max_depth_index,
+                                     float min_distance, int is_initial_query,
+                                     int32_t* query_indices, int16_t* assigned_networks,
+                                     nerf_stream_t stream);
+
+/* cuda/fourier_features.cu:8-100 — per scalar [x, cos(f_0 x)..cos(f_{L-1}x),
+ * sin(f_0 x)..sin(f_{L-1}x)], out [n*(2L+1)]. */
+int kn_compute_fourier_features(const float* input, int64_t n, const float* freqs, int L,
+                                float* out, nerf_stream_t stream);
+
+/* cuda/integrate.cu:9-81 — post-activation rgb_sigma [num_rays*spr][4],
+ * per-ray dists [num_rays]; rgb_map [num_rays][3] (the reference passes it as
+ * a raw int64 address), acc/T/mask in place. */
+int kn_integrate(const float* rgb_sigma, const float* dists, float* rgb_map, float* acc_map,
+                 float* transmittance, uint8_t* active_ray_mask, int num_rays,
+                 int samples_per_ray, float transmittance_threshold, int is_initial_query,
+                 nerf_stream_t stream);
+
+/* cuda/integrate.cu:83-112 — rgb += bg * (1 - acc), n pixels. */
+int kn_replace_transparency_by_background_color(float* rgb_map, const float* acc_map, int64_t n,
+                                                const float* background_color /* device [3] */,
+                                                nerf_stream_t stream);
+
+/* cuda/reorder.cu:13-49 */
+int kn_gather_int32(const int32_t* map, int64_t n_out, const int32_t* input, int32_t* out,
+                    nerf_stream_t stream);
+int kn_scatter_int32_float4(const int32_t* map, int64_t n, const float* input /*[n][4]*/,
+                            float* out /*[..][4]*/, nerf_stream_t stream);
+/* stable sort of (key, value) pairs by int16 key, in place; scratch: device
+ * bytes >= kn_sort_scratch_bytes(n, value_bytes). value_bytes = 4 or 8. */
+size_t kn_sort_scratch_bytes(int64_t n, int value_bytes);
+int kn_sort_by_key_int16(int16_t* keys, void* values, int value_bytes, int64_t n,
+                         void* scratch, nerf_stream_t stream);
+
+/* cuda/global_to_local.cu:8-62 — in place p = 2(p-min_k)/(max_k-min_k)-1 per
+ * network segment; batch_size_per_network is HOST memory (the reference reads
+ * it on the host, global_to_local.cu:36-47). */
+int kn_global_to_local(float* points, const float* domain_mins, const float* domain_maxs,
+                       const int64_t* batch_size_per_network_host, int num_networks,
+                       nerf_stream_t stream);
+
+/* cuda/network_eval.cu:24-297 — KiloNeRF tiny-MLP evaluation (hidden 32). */
+int kn_network_eval_query_index(const int32_t* query_indices, int64_t batch, const float* params,
+                                const float* domain_mins, const float* domain_maxs,
+                                const int32_t* starts, const int32_t* ends,
+                                const float* origin, const float* c2w, int num_networks,
+                                int hidden_dim, int H, int W, float cx, float cy, float fx,
+                                float fy, int max_depth_index, float min_distance,
+                                float distance_between_samples, float* out /*[batch][4]*/,
+                                nerf_stream_t stream);
+
+/* cuda/multimatmul.cu:18-100 — stream pool and MAGMA init (MAGMA is not used:
+ * the grouped GEMM is a native kernel; init_magma succeeds as a no-op). */
+int kn_init_stream_pool(int64_t num_streams);
+int kn_destroy_stream_pool(void);
+int kn_init_magma(void);
+
+/* cuda/multimatmul.cu:152-428 — grouped GEMM over consecutive row segments:
+ * for network k with b_k rows, out[rows_k][out_f] = X[rows_k][in_f] · op(W_k)
+ * (+ bias_k). The reference's MAGMA column-major views mean
+ *   mode 0 (static, with bias) / 1 (without bias): W_k stored [in_f][out_f];
+ *   mode 2 (without bias, transposed weights):     W_k stored [out_f][in_f].
+ * bias: [num_networks][out_f] (mode 0 only). batch_size_per_network is HOST
+ * memory (the reference reads it on the host). Handle = returned by init. */
+int kn_init_multimatmul_grouped(int64_t num_networks, int64_t out_features, int64_t in_features,
+                                const int32_t* group_limits, int n_group_limits, int* handle);
+int kn_deinit_multimatmul_grouped(int handle);
+int kn_multimatmul_grouped(int handle, int mode, const float* biases, const float* X,
+                           const float* W, int64_t out_features, int64_t in_features,
+                           const int64_t* batch_size_per_network_host, int num_networks,
+                           float* out, nerf_stream_t stream);
+
+/* cuda/multimatmul.cu:430-524 — per-network column sums of M [Σb][cols]. */
+int kn_multi_row_sum_reduction(const float* M, int64_t cols,
+                               const int64_t* batch_size_per_network_host, int num_networks,
+                               float* out /*[num_networks][cols]*/, nerf_stream_t stream);
+
+/* cuda/multimatmul.cu:527-623 — per-network A_k^T · B_k, A [Σb][a_cols],
+ * B [Σb][b_cols] -> out [num_networks][a_cols][b_cols]. */
+int kn_multimatmul_A_transposed(const float* A, int64_t a_cols, const float* B, int64_t b_cols,
+                                const int64_t* batch_size_per_network_host, int num_networks,
+                                float* out, nerf_stream_t stream);
+
+/* cuda/render_to_screen.cpp:222-248 — OpenGL viewer: not supported. */
+int kn_render_to_screen(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERFHIP_H */

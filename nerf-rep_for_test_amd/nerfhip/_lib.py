@@ -1,0 +1,108 @@
+"""ctypes binding of lib/libnerfhip.so (the C ABI declared in include/nerfhip.h).
+
+There is no fallback: if the library is missing or no ROCm device is present,
+``lib()`` raises, and so does every op built on it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("NERFHIP_LIB", os.path.join(PKG_ROOT, "lib", "libnerfhip.so"))
+
+MLP_SLICES = 73
+MLP_SLICE_FLOATS = 8192
+MLP_HEAD_FLOATS = 3200
+
+_P, _I, _I64, _F, _S, _SZ = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_void_p, C.c_size_t
+
+# name -> (restype, argtypes); mirrors include/nerfhip.h
+SIGNATURES = {
+    "nerf_last_error": (C.c_char_p, []),
+    "nerf_version": (_I, []),
+    "nerf_rays": (_I, [_P, _I, _I, _I64, _I64, _P, _P, _S]),
+    "nerf_sample_coarse": (_I, [_P, _P, _I64, _I, _P, _S]),
+    "nerf_mlp_forward": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
+    "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
+    "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _S]),
+    "nerf_sample_fine": (_I, [_P, _I64, _P, _P, _I64, _I64, _I, _I, _P, _S]),
+    "nerf_sample_coarse_ess": (_I, [_P, _P, _P, _I, _P, _P, _I64, _I, _I, _F, _P, _S]),
+    "nerf_grid_update": (_I, [_P, _P, _I64, _P, _P, _I64, _I, _P, _I, _S]),
+    "kn_get_rays_d": (_I, [_I, _I, _F, _F, _F, _F, _P, _P, _S]),
+    "kn_generate_query_indices_on_ray": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _F, _I, _I,
+                                              _F, _I, _P, _P, _S]),
+    "kn_compute_fourier_features": (_I, [_P, _I64, _P, _I, _P, _S]),
+    "kn_integrate": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _S]),
+    "kn_replace_transparency_by_background_color": (_I, [_P, _P, _I64, _P, _S]),
+    "kn_gather_int32": (_I, [_P, _I64, _P, _P, _S]),
+    "kn_scatter_int32_float4": (_I, [_P, _I64, _P, _P, _S]),
+    "kn_sort_scratch_bytes": (_SZ, [_I64, _I]),
+    "kn_sort_by_key_int16": (_I, [_P, _P, _I, _I64, _P, _S]),
+    "kn_global_to_local": (_I, [_P, _P, _P, _P, _I, _S]),
+    "kn_network_eval_query_index": (_I, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                         _F, _F, _F, _F, _I, _F, _F, _P, _S]),
+    "kn_init_stream_pool": (_I, [_I64]),
+    "kn_destroy_stream_pool": (_I, []),
+    "kn_init_magma": (_I, []),
+    "kn_init_multimatmul_grouped": (_I, [_I64, _I64, _I64, _P, _I, C.POINTER(C.c_int)]),
+    "kn_deinit_multimatmul_grouped": (_I, [_I]),
+    "kn_multimatmul_grouped": (_I, [_I, _I, _P, _P, _P, _I64, _I64, _P, _I, _P, _S]),
+    "kn_multi_row_sum_reduction": (_I, [_P, _I64, _P, _I, _P, _S]),
+    "kn_multimatmul_A_transposed": (_I, [_P, _I64, _P, _I64, _P, _I, _P, _S]),
+    "kn_render_to_screen": (_I, []),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NerfHipError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the library once (raises NerfHipError if it is not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NerfHipError(
+                    f"HIP library not found at {LIB_PATH}: build it with "
+                    "`make -C nerf-rep_for_test_amd` (or __graft_entry__.build())")
+            h = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        msg = lib().nerf_last_error().decode(errors="replace")
+        raise NerfHipError(f"{name} failed (code {rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t) -> int:
+    """Device (or host) address of a torch tensor, or None for None."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t) -> None:
+    if not t.is_cuda:
+        raise NerfHipError("nerfhip ops need tensors on a ROCm GPU (got %s); there is no CPU "
+                           "fallback" % t.device)

@@ -1,0 +1,300 @@
+"""GPU parity of the HIP render path against the CPU oracle and the golden vectors.
+
+Stage tests feed the HIP kernel and the oracle identical inputs; end-to-end
+tests render the golden fixtures' cameras. Tolerances (north_star): rgb/acc
+within 1e-5 abs, depth within 1e-5 relative to its magnitude, disp NaN-aware.
+Fine maps end-to-end are checked by PSNR (fine depths depend on float32 MLP
+rounding) and exactly-staged by feeding reference depths.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names
+from goldlib import grid_of, load, max_err, oracle_cfg, params_of, psnr, rel_err
+from oracle import nerf_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+ALL = golden_names()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _pipe(dev, z=None, **kw):
+    from nerfhip.render import NerfPipeline
+    if z is not None:
+        kw = dict(N_samples=int(z["N_samples"]), N_importance=int(z["N_importance"]),
+                  near=float(z["near"]), far=float(z["far"]), lindisp=bool(z["lindisp"]),
+                  white_bkgd=bool(z["white_bkgd"]), enable_ess=bool(z["enable_ess"]),
+                  enable_ert=bool(z["enable_ert"]), ert_threshold=float(z["ert_threshold"]), **kw)
+    return NerfPipeline(dev, **kw)
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+# ---------------------------------------------------------------- stages
+@pytest.mark.parametrize("name", ["f1_c2_crop", "f2b_c2_dense", "f6_ragged_lindisp"])
+def test_rays_bit_exact(dev, name):
+    z = load(name)
+    pipe = _pipe(dev, z)
+    ro, rd = pipe.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
+    oro, ord_ = O.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
+    assert np.array_equal(ro.cpu().numpy(), oro)
+    assert np.array_equal(rd.cpu().numpy(), ord_)
+
+
+def test_rays_row_band(dev):
+    """A row band [p0, p0+n) equals the same rows of the full image (tile sharding)."""
+    z = load("f1_c2_crop")
+    pipe = _pipe(dev, z)
+    H, W = int(z["H"]), int(z["W"])
+    full = pipe.camera_rays(H, W, z["pose"], z["K"])[1]
+    band = pipe.camera_rays(H, W, z["pose"], z["K"], p0=5 * W, n=7 * W)[1]
+    assert torch.equal(band, full[5 * W:12 * W])
+
+
+@pytest.mark.parametrize("n,S,stride0", [(1, 64, True), (3, 64, False), (37, 192, False),
+                                         (130, 64, True), (2, 7, False)])
+def test_mlp_matches_oracle(dev, n, S, stride0):
+    z = load("f1_c2_crop")
+    p = params_of(z)
+    rng = np.random.default_rng(n * 1000 + S)
+    ro = np.repeat(rng.uniform(-3, 3, (1, 3)), n, 0).astype(np.float32) + \
+        rng.normal(0, 0.1, (n, 3)).astype(np.float32)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    if stride0:
+        zz = np.sort(rng.uniform(2, 6, S)).astype(np.float32)
+        zr = np.broadcast_to(zz, (n, S))
+    else:
+        zr = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    pipe = _pipe(dev, N_samples=S, N_importance=0)
+    pipe.set_weights(p)
+    raw = pipe.mlp(pipe.coarse, _t(ro, dev), _t(rd, dev), _t(zz if stride0 else zr, dev),
+                   0 if stride0 else S, n, S).cpu().numpy().reshape(n, S, 4)
+    pts = (ro[:, None, :] + rd[:, None, :] * zr[:, :, None]).astype(np.float32)
+    ref = O.query_network(pts, rd, p, "model")
+    scale = np.maximum(1.0, np.abs(ref.reshape(-1, 4)).max(0))
+    assert (np.abs(raw - ref).reshape(-1, 4) / scale).max() < 1e-5
+
+
+def test_mlp_dense_weights(dev):
+    """gain-3 weights (large activations): same channel-relative bound."""
+    z = load("f2b_c2_dense")
+    p = params_of(z)
+    oro, ord_ = O.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
+    n = 200
+    zc = np.broadcast_to(O.coarse_depths(2.0, 6.0, 64, False), (n, 64))
+    pipe = _pipe(dev, N_samples=64, N_importance=0)
+    pipe.set_weights(p)
+    raw = pipe.mlp(pipe.coarse, _t(oro[:n], dev), _t(ord_[:n], dev), pipe.z_base, 0, n, 64)
+    pts = (oro[:n, None, :] + ord_[:n, None, :] * zc[:, :, None]).astype(np.float32)
+    ref = O.query_network(pts, ord_[:n], p, "model").reshape(-1, 4)
+    scale = np.maximum(1.0, np.abs(ref).max(0))
+    assert (np.abs(raw.cpu().numpy() - ref) / scale).max() < 1e-5
+
+
+def _rand_raw(rng, n, S, dense):
+    raw = rng.normal(0, 2.0, (n, S, 4)).astype(np.float32)
+    raw[..., 3] = rng.normal(2.0 if dense else -0.5, 3.0, (n, S)).astype(np.float32)
+    return raw
+
+
+@pytest.mark.parametrize("S,dense,white", [(64, False, True), (192, True, True), (64, True, False),
+                                           (5, True, True), (130, False, True)])
+def test_composite_given_raw(dev, S, dense, white):
+    rng = np.random.default_rng(S)
+    n = 777
+    raw = _rand_raw(rng, n, S, dense)
+    zr = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    pipe = _pipe(dev, N_samples=S, N_importance=0, white_bkgd=white)
+    out = pipe.alloc_outputs(n)["coarse"]
+    w = pipe.composite(_t(raw, dev), _t(zr, dev), S, _t(rd, dev), n, S, out, 0)
+    rgb, disp, acc, wt, depth = O.raw2outputs(raw, zr, rd, white)
+    # same op sequence and summation order; exp may differ by an ulp (SLEEF vs ocml)
+    assert max_err(w.cpu().numpy(), wt) < 1e-6
+    assert max_err(out[0].cpu().numpy(), rgb) < 1e-6
+    assert max_err(out[2].cpu().numpy(), acc) < 1e-6
+    assert rel_err(out[3].cpu().numpy(), depth) < 1e-6
+    assert rel_err(out[1].cpu().numpy(), disp, floor=1e-3) < 1e-5
+
+
+def test_composite_ert_chunks(dev):
+    """ERT with the chunk-wide argmax rule over 3 chunks (2048, 2048, 500 rays)."""
+    rng = np.random.default_rng(7)
+    n, S = 2048 * 2 + 500, 64
+    raw = _rand_raw(rng, n, S, True)
+    raw[2048:4096, :, 3] = -5.0          # chunk 1: nothing terminates -> weights kept
+    raw[2048 + 17, :, 3] = 50.0          # ... except one ray -> whole chunk cut
+    raw[4096:, :, 3] = -5.0              # chunk 2: nothing terminates at all
+    zr = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    pipe = _pipe(dev, N_samples=S, N_importance=0, enable_ert=True, ert_threshold=0.01)
+    out = pipe.alloc_outputs(n)["coarse"]
+    w = pipe.composite(_t(raw, dev), _t(zr, dev), S, _t(rd, dev), n, S, out, 0).cpu().numpy()
+    for c0 in range(0, n, 2048):
+        sl = slice(c0, min(n, c0 + 2048))
+        rgb, disp, acc, wt, depth = O.raw2outputs_ert(raw[sl], zr[sl], rd[sl], 0.01)
+        assert max_err(w[sl], wt) < 1e-6
+        assert max_err(out[0].cpu().numpy()[sl], rgb) < 1e-6
+        assert max_err(out[2].cpu().numpy()[sl], acc) < 1e-6
+        assert np.array_equal(np.isnan(out[1].cpu().numpy()[sl]), np.isnan(disp))
+
+
+@pytest.mark.parametrize("name", ["f1_c2_crop", "f2_c2_perturb", "f2b_c2_dense", "f3_ert"])
+def test_sample_fine_given_reference_weights(dev, name):
+    z = load(name)
+    zc, wc = z["int_zc"], z["int_wc"]
+    n, S = zc.shape
+    NI = int(z["N_importance"])
+    pipe = _pipe(dev, z)
+    zall = torch.empty((n, S + NI), device=dev)
+    from nerfhip._lib import call, ptr, stream_of
+    call("nerf_sample_fine", ptr(_t(zc, dev)), S, ptr(_t(wc, dev)), ptr(pipe.u_eval), 0, n, S, NI,
+         ptr(zall), stream_of(dev))
+    mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
+    ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1],
+                                                   O.linspace_f32(0, 1, NI))], -1), -1)
+    got = zall.cpu().numpy()
+    assert np.array_equal(got, ref)                   # identical inputs: bit-exact
+    err = np.abs(got - z["int_zall"]).max(-1)         # vs the reference's own depths
+    assert np.mean(err < 1e-5) >= 0.97
+
+
+def test_sample_fine_training_u(dev):
+    """Training-mode u (unsorted uniform draws, VR:247-249)."""
+    rng = np.random.default_rng(3)
+    n, S, NI = 300, 64, 128
+    zc = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    wc = (rng.random((n, S)) ** 4).astype(np.float32)
+    u = rng.random((n, NI)).astype(np.float32)
+    zall = torch.empty((n, S + NI), device=dev)
+    from nerfhip._lib import call, ptr, stream_of
+    call("nerf_sample_fine", ptr(_t(zc, dev)), S, ptr(_t(wc, dev)), ptr(_t(u, dev)), NI, n, S, NI,
+         ptr(zall), stream_of(dev))
+    mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
+    ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1], u)], -1), -1)
+    assert np.array_equal(zall.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("name", ["f4_ess_ert", "f4b_ess_ert_update"])
+def test_ess_depths_given_grid(dev, name):
+    z = load(name)
+    grid = grid_of(z)
+    H, W = int(z["H"]), int(z["W"])
+    oro, ord_ = O.camera_rays(H, W, z["pose"], z["K"])
+    n = oro.shape[0]
+    tr = z["t_rand"] if "t_rand" in z else None
+    pipe = _pipe(dev, z)
+    pipe.set_grid(grid)
+    zz = torch.empty((n, 64), device=dev)
+    from nerfhip._lib import call, ptr, stream_of
+    call("nerf_sample_coarse_ess", ptr(_t(oro, dev)), ptr(_t(ord_, dev)), ptr(pipe.grid), 128,
+         ptr(pipe.z_base), ptr(None if tr is None else _t(tr, dev)), n, 64, 2048, 0.5, ptr(zz),
+         stream_of(dev))
+    for c0 in range(0, n, 2048):
+        sl = slice(c0, min(n, c0 + 2048))
+        ref = O.sample_coarse_ess(oro[sl], ord_[sl], grid, 2.0, 6.0, 64, False,
+                                  float(z["perturb"]), None if tr is None else tr[sl])
+        assert np.array_equal(zz.cpu().numpy()[sl], ref)
+    assert np.array_equal(zz.cpu().numpy()[:z["int_zc"].shape[0]], z["int_zc"])
+
+
+# ---------------------------------------------------------------- end to end
+def _render_fixture(dev, z):
+    pipe = _pipe(dev, z)
+    pipe.set_weights(params_of(z))
+    g = grid_of(z)
+    if g is not None:
+        pipe.set_grid(g)
+    pipe.grid_update_counter = int(z["grid_counter_in"])
+    tr = _t(z["t_rand"], dev) if "t_rand" in z else None
+    res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"], t_rand=tr)
+    return pipe, {k: v.cpu().numpy() for k, v in res.items()}
+
+
+@pytest.mark.parametrize("name", ALL)
+def test_render_coarse_maps_vs_golden(dev, name):
+    z = load(name)
+    pipe, res = _render_fixture(dev, z)
+    n = int(z["H"]) * int(z["W"])
+    assert max_err(res["rgb_map_0"], z["out_rgb_map_0"].reshape(n, 3)) < TOL
+    assert max_err(res["acc_map_0"], z["out_acc_map_0"].reshape(n)) < TOL
+    assert rel_err(res["depth_map_0"], z["out_depth_map_0"].reshape(n)) < TOL
+    assert rel_err(res["disp_map_0"], z["out_disp_map_0"].reshape(n), floor=1e-3) < 1e-4
+    assert pipe.grid_update_counter == int(z["grid_counter_out"])
+    if "grid_out_packed" in z:
+        g = pipe.grid.cpu().numpy().astype(bool)
+        assert np.array_equal(np.packbits(g), z["grid_out_packed"])
+
+
+@pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5")])
+def test_render_fine_maps_psnr_vs_golden(dev, name):
+    z = load(name)
+    _, res = _render_fixture(dev, z)
+    n = int(z["H"]) * int(z["W"])
+    assert psnr(res["rgb_map"], z["out_rgb_map"].reshape(n, 3)) > 35.0
+
+
+@pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5")])
+def test_fine_pass_given_reference_depths(dev, name):
+    """Fine MLP + composite on the reference's own fine depths: 1e-5."""
+    z = load(name)
+    zall = z["int_zall"]
+    n, S2 = zall.shape
+    oro, ord_ = O.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
+    pipe = _pipe(dev, z)
+    pipe.set_weights(params_of(z))
+    ro, rd = _t(oro[:n], dev), _t(ord_[:n], dev)
+    zt = _t(zall, dev)
+    raw = pipe.mlp(pipe.fine, ro, rd, zt, S2, n, S2)
+    out = pipe.alloc_outputs(n)["coarse"]
+    if bool(z["enable_ert"]) and not bool(z["int_chunk_any_1"]):
+        pytest.skip("sub-chunk slice cannot reproduce a no-termination chunk decision")
+    pipe.composite(raw, zt, S2, rd, n, S2, out, 0)
+    ref = {k: z["out_" + k].reshape(int(z["H"]) * int(z["W"]), -1)[:n] for k in
+           ("rgb_map", "acc_map", "depth_map", "disp_map")}
+    if bool(z["enable_ert"]) and not (ref["acc_map"] > 0).all():
+        pass
+    assert max_err(out[0].cpu().numpy(), ref["rgb_map"]) < TOL
+    assert max_err(out[2].cpu().numpy(), ref["acc_map"][:, 0]) < TOL
+    assert rel_err(out[3].cpu().numpy(), ref["depth_map"][:, 0]) < TOL
+
+
+def test_renderer_plugin_contract(dev):
+    """src.models.nerf.renderer.volume_renderer.Renderer(net).render(batch) -> 8 maps."""
+    from src.config import cfg, reset
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    from nerfhip.synthetic import load_into_network
+    z = load("f1_c2_crop")
+    reset()
+    cfg.task_arg.perturb = 0
+    cfg.enable_ess = False
+    cfg.enable_ert = False
+    net = Network().to(dev)
+    load_into_network(net, params_of(z))
+    net.eval()
+    rend = Renderer(net)
+    batch = {"H": int(z["H"]), "W": int(z["W"]), "pose": torch.from_numpy(z["pose"])[None],
+             "intrinsics": torch.from_numpy(z["K"])[None]}
+    with torch.no_grad():
+        out = rend.render(batch)
+    assert set(out) == {"rgb_map_0", "disp_map_0", "acc_map_0", "depth_map_0",
+                        "rgb_map", "disp_map", "acc_map", "depth_map"}
+    assert out["rgb_map"].shape == (32, 32, 3) and out["acc_map"].shape == (32, 32)
+    assert out["rgb_map"].device.type == "cuda"
+    assert max_err(out["rgb_map_0"].cpu().numpy(), z["out_rgb_map_0"]) < TOL
+    reset()
