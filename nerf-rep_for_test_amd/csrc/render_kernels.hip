@@ -227,20 +227,22 @@ __global__ __launch_bounds__(FINE_BLOCK) void sample_fine_kernel(
     zf[j] = bg0 + tt * (bg1 - bg0);
   }
   // torch.sort(cat(z, zf)) (values only): insertion-sort zf (already ascending
-  // in eval mode), then merge with the ascending coarse row from the back, in
-  // place: the write index a+b-1 never passes the read index S+b-1.
+  // in eval mode), then merge it with the ascending coarse row front to back,
+  // in place: while coarse values remain (a < S) the write index a+b stays
+  // below the first unread fine sample at S+b; once they are exhausted the
+  // remaining fine samples already sit at their final positions.
   for (int j = 1; j < n_imp; ++j) {
     const float v = zf[j];
     int k = j - 1;
     while (k >= 0 && zf[k] > v) { zf[k + 1] = zf[k]; --k; }
     zf[k + 1] = v;
   }
-  int a = S, b = n_imp;
-  while (a > 0 && b > 0) {
-    const float za = zr[a - 1], zb = zf[b - 1];
-    if (zb > za) { out[a + b - 1] = zb; --b; } else { out[a + b - 1] = za; --a; }
+  int a = 0, b = 0;
+  while (a < S && b < n_imp) {
+    const float za = zr[a], zb = zf[b];
+    if (zb < za) { out[a + b] = zb; ++b; } else { out[a + b] = za; ++a; }
   }
-  while (a > 0) { out[a - 1] = zr[a - 1]; --a; }
+  while (a < S) { out[a + b] = zr[a]; ++a; }
 }
 
 // ---------------------------------------------------------------------------

@@ -157,8 +157,9 @@ def sort_by_key_int16_int32(keys_tensor, values_tensor):
 def get_rays_d(H, W, cx, cy, fx, fy, c2w_tensor, root_num_blocks, root_num_threads):
     _gpu(c2w_tensor)
     out = torch.empty((int(H), int(W), 3), device=c2w_tensor.device, dtype=torch.float32)
+    c2w = c2w_tensor.contiguous()            # held until the launch is enqueued
     call("kn_get_rays_d", int(H), int(W), float(cx), float(cy), float(fx), float(fy),
-         ptr(c2w_tensor.contiguous()), ptr(out), _st(c2w_tensor))
+         ptr(c2w), ptr(out), _st(c2w_tensor))
     return out
 
 
@@ -198,8 +199,8 @@ def compute_fourier_features(input_tensor, frequency_bands_tensor, kernel_max_nu
     n = input_tensor.numel()
     L = frequency_bands_tensor.numel()
     out = torch.empty((n * (2 * L + 1),), device=input_tensor.device, dtype=torch.float32)
-    call("kn_compute_fourier_features", ptr(input_tensor.contiguous()), n,
-         ptr(frequency_bands_tensor.contiguous()), L, ptr(out), _st(input_tensor))
+    x, f = input_tensor.contiguous(), frequency_bands_tensor.contiguous()
+    call("kn_compute_fourier_features", ptr(x), n, ptr(f), L, ptr(out), _st(input_tensor))
     return out
 
 
@@ -237,8 +238,9 @@ def replace_transparency_by_background_color(rgb_map_pointer, acc_map_tensor,
     """acc_map must be [H, W] (the reference reads size(0)*size(1), integrate.cu:105)."""
     _gpu(acc_map_tensor, background_color_tensor)
     n = acc_map_tensor.size(0) * acc_map_tensor.size(1)
+    bg = background_color_tensor.contiguous()
     call("kn_replace_transparency_by_background_color", int(rgb_map_pointer), ptr(acc_map_tensor),
-         n, ptr(background_color_tensor.contiguous()), _st(acc_map_tensor))
+         n, ptr(bg), _st(acc_map_tensor))
 
 
 # ---------------------------------------------------------------- render_to_screen.h

@@ -91,7 +91,11 @@ def call(name: str, *args) -> None:
 
 
 def ptr(t) -> int:
-    """Device (or host) address of a torch tensor, or None for None."""
+    """Device (or host) address of a torch tensor, or None for None.
+
+    The caller must keep ``t`` referenced until the call using the address has
+    been enqueued: the address of a temporary (``ptr(x.contiguous())``) can be
+    handed to the next allocation by torch's caching allocator."""
     if t is None:
         return None
     return t.data_ptr()

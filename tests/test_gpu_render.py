@@ -162,7 +162,8 @@ def test_sample_fine_given_reference_weights(dev, name):
     pipe = _pipe(dev, z)
     zall = torch.empty((n, S + NI), device=dev)
     from nerfhip._lib import call, ptr, stream_of
-    call("nerf_sample_fine", ptr(_t(zc, dev)), S, ptr(_t(wc, dev)), ptr(pipe.u_eval), 0, n, S, NI,
+    zc_d, wc_d = _t(zc, dev), _t(wc, dev)          # keep the inputs alive across the call
+    call("nerf_sample_fine", ptr(zc_d), S, ptr(wc_d), ptr(pipe.u_eval), 0, n, S, NI,
          ptr(zall), stream_of(dev))
     mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
     ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1],
@@ -182,8 +183,9 @@ def test_sample_fine_training_u(dev):
     u = rng.random((n, NI)).astype(np.float32)
     zall = torch.empty((n, S + NI), device=dev)
     from nerfhip._lib import call, ptr, stream_of
-    call("nerf_sample_fine", ptr(_t(zc, dev)), S, ptr(_t(wc, dev)), ptr(_t(u, dev)), NI, n, S, NI,
-         ptr(zall), stream_of(dev))
+    zc_d, wc_d, u_d = _t(zc, dev), _t(wc, dev), _t(u, dev)
+    call("nerf_sample_fine", ptr(zc_d), S, ptr(wc_d), ptr(u_d), NI, n, S, NI, ptr(zall),
+         stream_of(dev))
     mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
     ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1], u)], -1), -1)
     assert np.array_equal(zall.cpu().numpy(), ref)
@@ -201,9 +203,10 @@ def test_ess_depths_given_grid(dev, name):
     pipe.set_grid(grid)
     zz = torch.empty((n, 64), device=dev)
     from nerfhip._lib import call, ptr, stream_of
-    call("nerf_sample_coarse_ess", ptr(_t(oro, dev)), ptr(_t(ord_, dev)), ptr(pipe.grid), 128,
-         ptr(pipe.z_base), ptr(None if tr is None else _t(tr, dev)), n, 64, 2048, 0.5, ptr(zz),
-         stream_of(dev))
+    ro_d, rd_d = _t(oro, dev), _t(ord_, dev)
+    tr_d = None if tr is None else _t(tr, dev)
+    call("nerf_sample_coarse_ess", ptr(ro_d), ptr(rd_d), ptr(pipe.grid), 128, ptr(pipe.z_base),
+         ptr(tr_d), n, 64, 2048, 0.5, ptr(zz), stream_of(dev))
     for c0 in range(0, n, 2048):
         sl = slice(c0, min(n, c0 + 2048))
         ref = O.sample_coarse_ess(oro[sl], ord_[sl], grid, 2.0, 6.0, 64, False,
