@@ -2,162 +2,309 @@
 // reference src/models/nerf/network.py:49-74 (NET), FP32 MFMA.
 //
 // Work decomposition
-//   workgroup = 4 waves = 128 consecutive samples (sample = ray * S + step);
-//   wave = 32 samples = the N dimension of v_mfma_f32_32x32x2_f32.
-//   Every layer is out^T[F x 32] = W[F x K] . in^T[K x 32]: weights are the
-//   A operand (rows = output features), activations the B operand.
+//   workgroup = 8 waves (2 per SIMD) = 128 consecutive samples
+//   (sample = ray * S + step); wave = 16 samples = the N dimension of
+//   v_mfma_f32_16x16x4_f32. Every layer is out^T[F x 16] = W[F x K] . in^T[K x 16]:
+//   weights are the A operand (rows = output features), activations the B operand.
 //
 // Register dataflow (no LDS round trip for activations)
-//   The 32x32 accumulator of output tile m holds, on lane l, sample l&31 and
-//   output features 32m + (r&3) + 8(r>>2) + 4(l>>5) in register r (0..15).
-//   The next layer consumes register r of tile m as its B operand at k-step
-//   s = 16m + r: lane half h = l>>5 supplies K index "slot h" of that step. The
-//   host packs each weight matrix with exactly that K permutation
-//   (nerfhip/pack.py), so accumulators feed the next MFMA chain in place.
-//   Encoded inputs use their own K order: k-step 0 = (x | y), 1 = (z | 0),
-//   2+3f+c = (sin(2^f p_c) | cos(2^f p_c)).
+//   The 16x16 accumulator of output tile m holds, on lane l, sample l&15 and
+//   output features 16m + 4(l>>4) + r in register r (0..3). The next layer
+//   consumes register r of tile m as its B operand at k-step s = 4m + r: lane
+//   group g4 = l>>4 supplies K slot g4 of that step. The host packs each weight
+//   matrix with exactly that K permutation (nerfhip/pack.py), so accumulators
+//   feed the next MFMA chain in place. Encoded inputs use their own K order:
+//   k-step 0 = (x, y, z, 0), 1+t = (sin a, cos a, sin b, cos b) for the
+//   (band, coordinate) pairs a = 2t, b = 2t+1.
+//   Per wave: 64 activation VGPRs + 64 accumulator AGPRs, so two waves fit per
+//   SIMD and fragment reads are prefetched one MFMA group ahead.
 //
 // Weight streaming
 //   The packed network is 73 slices of 32 KiB (32 "blocks" of 64 lanes x 16 B:
-//   one ds_read_b128 per lane = 4 consecutive k-steps of one 32-row tile).
-//   Slices stream HBM/L2 -> LDS with global_load_lds_dwordx4 into a 2-deep
-//   ring (two LDS arrays, statically selected), one barrier per slice; 128
-//   MFMAs (8192 cycles per SIMD) per slice hide the next slice's load.
-//   Density (1x256) and rgb (3x128) heads run on the VALU (fma chains + one
-//   cross-half add) instead of padding 31/29 of 32 MFMA rows.
+//   one ds_read_b128 per lane = 4 consecutive k-steps of one 16-row tile).
+//   Slices stream L2 -> LDS with global_load_lds_dwordx4 into a 2-deep ring
+//   (two LDS arrays, statically selected), one barrier per slice; 128 MFMAs per
+//   wave (2 x 4096 cycles per SIMD) per slice hide the next slice's load.
+//   Density (1x256) and rgb (3x128) heads run on the VALU (fma chains + a
+//   4-lane butterfly) instead of padding 15/13 of 16 MFMA rows.
 #include "common.h"
 
 namespace nerfhip {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 256;
-constexpr int kTile = 128;
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTile = 16 * kWaves;            // samples per workgroup
 constexpr int kSliceFloats = NERF_MLP_SLICE_FLOATS;
 constexpr int kSlices = NERF_MLP_SLICES;
 constexpr int kHeadFloats = NERF_MLP_HEAD_FLOATS;
+constexpr int kBlocksPerWave = 32 / kWaves;   // glds pieces each wave stages per slice
 
-// head block layout (floats); bias/weight vectors are lane-half packed:
-// element [h][16m + r] belongs to output feature 32m + (r&3) + 8(r>>2) + 4h.
-constexpr int kHeadBias = 0;          // layers 0..8 (pts 0..7, feature): [9][2][128]
-constexpr int kHeadBiasViews = 2304;  // [2][64]
-constexpr int kHeadAlphaW = 2432;     // [2][128]
+// head block layout (floats); bias/weight vectors are lane-group packed:
+// element [g4][4m + r] belongs to output feature 16m + 4*g4 + r.
+constexpr int kHeadBias = 0;          // layers 0..8 (pts 0..7, feature): [9][4][64]
+constexpr int kHeadBiasViews = 2304;  // [4][32]
+constexpr int kHeadAlphaW = 2432;     // [4][64]
 constexpr int kHeadAlphaB = 2688;     // [1]
-constexpr int kHeadRgbW = 2692;       // [3][2][64]
+constexpr int kHeadRgbW = 2692;       // [3][4][32]
 constexpr int kHeadRgbB = 3076;       // [3]
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-__device__ __forceinline__ void stage_slice(const float4* __restrict__ slices, int g,
-                                            float* dst, int wave, int lane) {
-  if (g >= kSlices) return;
-  const float4* src = slices + (size_t)g * (kSliceFloats / 4);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int b = wave * 8 + j;
-    __builtin_amdgcn_global_load_lds((const void*)(src + b * 64 + lane),
-                                     (lds_ptr_t)(dst + b * 256), 16, 0, 0);
-  }
-  // keep the DMA issue ahead of this slice's MFMAs (the scheduler would
-  // otherwise sink it to the barrier and expose its latency)
-  __builtin_amdgcn_sched_barrier(0);
+// Ablation switches for timing-only builds (tools/mlp_ablate.py); the shipped
+// library defines none of them. ABL_NOBAR drops the per-slice barriers,
+// ABL_NODMA the weight staging, ABL_NOENC the sin/cos, ABL_NOEPI the bias/ReLU.
+// One 1-KiB LDS-DMA piece (of the 4 each wave stages per slice): block
+// wave*4 + j of slice `src` into the same block of LDS buffer `dst`.
+__device__ __forceinline__ void stage_piece(const float4* src, float* dst, int wave, int lane,
+                                            int j) {
+#if defined(ABL_NODMA)
+  return;
+#endif
+  const int b = wave * kBlocksPerWave + j;
+  __builtin_amdgcn_global_load_lds((const void*)(src + b * 64 + lane),
+                                   (lds_ptr_t)(dst + b * 256), 16, 0, 0);
 }
+
+// DMA of one future slice, spread over the MFMA groups of the current one.
+struct Dma {
+  const float4* src;   // slice in HBM/L2, or nullptr when there is none to stage
+  float* dst;          // its LDS ring buffer
+  int wave, lane;
+};
 
 __device__ __forceinline__ float4 frag(const float* buf, int block, int lane) {
   return *reinterpret_cast<const float4*>(buf + (block * 64 + lane) * 4);
 }
 
-#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+#define SCHED_DS_READ 0x100
+#define SCHED_MFMA 0x008
 
-// 256-row layer slice: 4 quads x 8 tiles, B operand = 16 k-steps in bv.
-__device__ __forceinline__ void slice256(f32x16 (&acc)[8], const float* buf, const f32x16& bv,
-                                         int lane) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float4 a = frag(buf, q * 8 + m, lane);
-      acc[m] = MFMA(a.x, bv[4 * q + 0], acc[m]);
-      acc[m] = MFMA(a.y, bv[4 * q + 1], acc[m]);
-      acc[m] = MFMA(a.z, bv[4 * q + 2], acc[m]);
-      acc[m] = MFMA(a.w, bv[4 * q + 3], acc[m]);
+// One group = 8 MFMAs: two 16-row tiles x the 4 k-steps of one quad.
+__device__ __forceinline__ void mfma_group(f32x4& c0, f32x4& c1, const float4& a0,
+                                           const float4& a1, const f32x4& bv) {
+  c0 = MFMA(a0.x, bv[0], c0);
+  c1 = MFMA(a1.x, bv[0], c1);
+  c0 = MFMA(a0.y, bv[1], c0);
+  c1 = MFMA(a1.y, bv[1], c1);
+  c0 = MFMA(a0.z, bv[2], c0);
+  c1 = MFMA(a1.z, bv[2], c1);
+  c0 = MFMA(a0.w, bv[3], c0);
+  c1 = MFMA(a1.w, bv[3], c1);
+}
+
+// LDS fragment reads are issued as inline asm: hipcc neither tracks nor waits
+// for them, so the schedule below owns every lgkmcnt wait of the slice loop
+// (hipcc's own waits there are lgkmcnt(0) placed after the next group's reads,
+// which serialises the LDS latency with the MFMAs). One per-lane base address
+// per buffer; the block offset is an instruction immediate.
+__device__ __forceinline__ unsigned lds_base(const float* buf, int lane) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(buf) +
+         (unsigned)(lane * 16);
+}
+
+template <int BLOCK>
+__device__ __forceinline__ float4 frag_async(unsigned base) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(BLOCK * 1024) : "memory");
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void lds_drain() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);   // keep MFMAs behind the wait (guide rule 18)
+}
+
+// Group G of NG over blocks 2G, 2G+1: drain group G's reads (issued one group
+// earlier), issue group G+1's into the other named register pair, then group
+// G's 8 MFMAs into tiles TILE(G), TILE(G)+1 with B operands BSEL(G).
+template <int G, int NG, typename Cfg, typename Acc, typename BV>
+__device__ __forceinline__ void run_group(Acc& acc, unsigned base, const BV& bv, float4& x0,
+                                          float4& x1, float4& y0, float4& y1, const Dma& dma) {
+  if constexpr (G < NG) {
+    lds_drain();
+    if constexpr ((G & 1) == 0 && G < 2 * kBlocksPerWave) {
+      if (dma.src) stage_piece(dma.src, dma.dst, dma.wave, dma.lane, G / 2);
     }
+    if constexpr (G + 1 < NG) {
+      if constexpr ((G & 1) == 0) {
+        y0 = frag_async<2 * G + 2>(base);
+        y1 = frag_async<2 * G + 3>(base);
+      } else {
+        x0 = frag_async<2 * G + 2>(base);
+        x1 = frag_async<2 * G + 3>(base);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int m = Cfg::tile(G);
+    if constexpr ((G & 1) == 0)
+      mfma_group(acc[m], acc[m + 1], x0, x1, bv[Cfg::bsel(G)]);
+    else
+      mfma_group(acc[m], acc[m + 1], y0, y1, bv[Cfg::bsel(G)]);
+    __builtin_amdgcn_sched_barrier(0);
+    run_group<G + 1, NG, Cfg>(acc, base, bv, x0, x1, y0, y1, dma);
   }
 }
 
-// 128-row layer slice: NQ quads x 4 tiles; k-steps from b0 (quads 0..3), b1 (4..7).
-template <int NQ>
-__device__ __forceinline__ void slice128(f32x16 (&acc)[4], const float* buf, const f32x16& b0,
-                                         const f32x16& b1, int lane) {
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const f32x16& bv = q < 4 ? b0 : b1;
-    const int qq = q & 3;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float4 a = frag(buf, q * 4 + m, lane);
-      acc[m] = MFMA(a.x, bv[4 * qq + 0], acc[m]);
-      acc[m] = MFMA(a.y, bv[4 * qq + 1], acc[m]);
-      acc[m] = MFMA(a.z, bv[4 * qq + 2], acc[m]);
-      acc[m] = MFMA(a.w, bv[4 * qq + 3], acc[m]);
-    }
-  }
+template <int NG, typename Cfg, typename Acc, typename BV>
+__device__ __forceinline__ void run_groups(Acc& acc, const float* buf, int lane, const BV& bv,
+                                           const Dma& dma) {
+  const unsigned base = lds_base(buf, lane);
+  float4 x0 = frag_async<0>(base), x1 = frag_async<1>(base);
+  float4 y0 = x0, y1 = x1;
+  run_group<0, NG, Cfg>(acc, base, bv, x0, x1, y0, y1, dma);
 }
 
-// Frequency encoding in the kernel's K order (see header). p: input 3-vector;
-// nf bands; out: 2 + 3*nf k-steps (rest zero). Lane half h picks sin|cos.
+// Slice shapes: which accumulator tiles and B-operand vectors group g uses.
+// 256-row layers: 2 quads x 16 tiles (quad g>>3, tiles 2(g&7), +1);
+// 128-row layers: 4 quads x 8 tiles (quad g>>2, tiles 2(g&3), +1).
+template <int QBASE>
+struct Slice256 {
+  static constexpr int tile(int g) { return 2 * (g & 7); }
+  static constexpr int bsel(int g) { return QBASE + (g >> 3); }
+};
+template <int QBASE>
+struct Slice128 {
+  static constexpr int tile(int g) { return 2 * (g & 3); }
+  static constexpr int bsel(int g) { return QBASE + (g >> 2); }
+};
+
+// 256-row layer slice SL of a layer (B operand vectors b[2*SL], b[2*SL+1]).
+template <int SL, typename BV>
+__device__ __forceinline__ void slice256(f32x4 (&acc)[16], const float* buf, const BV& b,
+                                         int lane, const Dma& dma) {
+  run_groups<16, Slice256<2 * SL>>(acc, buf, lane, b, dma);
+}
+
+// 128-row layer slice of NQ quads starting at B operand vector Q0.
+template <int NQ, int Q0, typename BV>
+__device__ __forceinline__ void slice128(f32x4 (&acc)[8], const float* buf, const BV& b,
+                                         int lane, const Dma& dma) {
+  run_groups<4 * NQ, Slice128<Q0>>(acc, buf, lane, b, dma);
+}
+
+// 4-deep slice ring: while slice g is computed, slices g+1 and g+2 are landed
+// or landing and slice g+3 is being staged into buffer (g+3)%4 (freed by the
+// barrier that ended slice g-1). At the end of slice g each wave waits only for
+// its own DMA of slice g+1 (counted vmcnt: the pieces of g+2 and g+3 may stay
+// in flight), then one raw s_barrier makes slice g+1 visible to all waves.
+struct Ring {
+  float* base;                     // 4 x kSliceFloats
+  const float4* slices;            // packed network in HBM
+  int wave, lane;
+  __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
+  __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
+    const int t = g + 3;
+    return Dma{t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t), wave,
+               lane};
+  }
+};
+
+template <int PENDING>   // slices (of 4 pieces) allowed to stay in flight
+__device__ __forceinline__ void slice_end() {
+#if !defined(ABL_NOBAR)
+  if constexpr (PENDING >= 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (PENDING == 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#endif
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Frequency encoding in the kernel's K order (see header) for lane group g4.
+// NF bands -> 1 + ceil(3*NF/2) k-steps, zero padded to 4*NV.
 template <int NF, int NV>
-__device__ __forceinline__ void encode(const float (&p)[3], int h, f32x16 (&out)[NV]) {
+__device__ __forceinline__ void encode(const float (&p)[3], int g4, f32x4 (&out)[NV]) {
 #pragma unroll
-  for (int v = 0; v < NV; ++v) out[v] = f32x16(0.0f);
-  out[0][0] = h ? p[1] : p[0];
-  out[0][1] = h ? 0.0f : p[2];
+  for (int v = 0; v < NV; ++v) out[v] = f32x4(0.0f);
+  out[0][0] = g4 == 0 ? p[0] : (g4 == 1 ? p[1] : (g4 == 2 ? p[2] : 0.0f));
+  constexpr int NPAIR = 3 * NF;
 #pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const float scale = (float)(1 << f);      // 2^f exact: x * 2^f is exact
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const int s = 2 + 3 * f + c;
-      const float arg = p[c] * scale;
+  for (int t = 0; 2 * t < NPAIR; ++t) {
+    const int pa = 2 * t + (g4 >> 1);        // (band, coordinate) pair of this lane group
+    float v = 0.0f;
+    if (pa < NPAIR) {
+      const int f = pa / 3, c = pa - 3 * (pa / 3);
+      const float x = c == 0 ? p[0] : (c == 1 ? p[1] : p[2]);
+      const float arg = x * (float)(1 << f);    // 2^f exact: x * 2^f is exact
+#if defined(ABL_NOENC)
+      v = arg;
+#else
       float sv, cv;
       sincosf(arg, &sv, &cv);
-      out[s >> 4][s & 15] = h ? cv : sv;
+      v = (g4 & 1) ? cv : sv;
+#endif
     }
+    out[(1 + t) >> 2][(1 + t) & 3] = v;
   }
 }
 
-__device__ __forceinline__ void bias_act(f32x16 (&act)[8], const f32x16 (&acc)[8],
+template <int T>
+__device__ __forceinline__ void bias_act(f32x4 (&act)[T], const f32x4 (&acc)[T],
                                          const float* bias, bool relu) {
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
+  for (int m = 0; m < T; ++m) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = acc[m][r] + bias[16 * m + r];
+    for (int r = 0; r < 4; ++r) {
+#if defined(ABL_NOEPI)
+      act[m][r] = acc[m][r];
+      (void)bias; (void)relu;
+#else
+      const float v = acc[m][r] + bias[4 * m + r];
       act[m][r] = relu ? fmaxf(v, 0.0f) : v;
+#endif
     }
   }
 }
 
-__global__ __launch_bounds__(kThreads, 1) void mlp_fused_kernel(
+// The 8 slices g .. g+7 of a 256-wide input layer (B = previous activations).
+__device__ __forceinline__ void layer_body(f32x4 (&acc)[16], const f32x4 (&act)[16],
+                                           const Ring& R, int g) {
+  slice256<0>(acc, R.buf(g + 0), act, R.lane, R.dma_for(g + 0)); slice_end<2>();
+  slice256<1>(acc, R.buf(g + 1), act, R.lane, R.dma_for(g + 1)); slice_end<2>();
+  slice256<2>(acc, R.buf(g + 2), act, R.lane, R.dma_for(g + 2)); slice_end<2>();
+  slice256<3>(acc, R.buf(g + 3), act, R.lane, R.dma_for(g + 3)); slice_end<2>();
+  slice256<4>(acc, R.buf(g + 4), act, R.lane, R.dma_for(g + 4)); slice_end<2>();
+  slice256<5>(acc, R.buf(g + 5), act, R.lane, R.dma_for(g + 5)); slice_end<2>();
+  slice256<6>(acc, R.buf(g + 6), act, R.lane, R.dma_for(g + 6)); slice_end<2>();
+  slice256<7>(acc, R.buf(g + 7), act, R.lane, R.dma_for(g + 7)); slice_end<2>();
+}
+
+// sum over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48);
+// every lane of the quad ends with the bitwise-same value
+__device__ __forceinline__ float quad_sum(float v) {
+  v = v + __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+__global__ __launch_bounds__(kThreads, 2) void mlp_fused_kernel(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
     float4* __restrict__ raw) {
-  __shared__ __attribute__((aligned(16))) float ring0[kSliceFloats];
-  __shared__ __attribute__((aligned(16))) float ring1[kSliceFloats];
+  __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
   __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int h = lane >> 5;
+  const int g4 = lane >> 4;
+  const Ring R{ring, slices, wave, lane};
 
-  stage_slice(slices, 0, ring0, wave, lane);
+  // prologue: slices 0, 1, 2 in flight; slice 3 is staged while slice 0 runs
+  for (int t = 0; t < 3; ++t)
+    for (int j = 0; j < kBlocksPerWave; ++j)
+      stage_piece(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane, j);
   for (int i = tid; i < kHeadFloats / 4; i += kThreads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
-  // this lane's sample (lanes l and l+32 share sample l&31)
-  const int64_t gs = (int64_t)blockIdx.x * kTile + wave * 32 + (lane & 31);
+  // this lane's sample (the 4 lanes l, l+16, l+32, l+48 share sample l&15)
+  const int64_t gs = (int64_t)blockIdx.x * kTile + wave * 16 + (lane & 15);
   const bool valid = gs < total;
   const int64_t gc = valid ? gs : total - 1;
   const int64_t ray = gc / S;
@@ -169,95 +316,74 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_fused_kernel(
     dv[c] = rays_d[ray * 3 + c];
     p[c] = rays_o[ray * 3 + c] + dv[c] * zv;      // VR:165: o + d*z, two roundings
   }
-  f32x16 enc[2];
-  encode<10, 2>(p, h, enc);
+  f32x4 enc[4];
+  encode<10, 4>(p, g4, enc);
 
-  f32x16 acc[8], act[8];
-  __syncthreads();   // slice 0 + head resident
+  f32x4 acc[16], act[16];
+  __syncthreads();   // head, z/rays loads and all three prologue slices resident
 
-  // ---- layer 0: 63 -> 256 (2 slices) --------------------------------------
+  // ---- layer 0: 63 -> 256 (slices 0, 1) ------------------------------------
 #pragma unroll
-  for (int m = 0; m < 8; ++m) acc[m] = f32x16(0.0f);
-  stage_slice(slices, 1, ring1, wave, lane);
-  slice256(acc, ring0, enc[0], lane);
-  __syncthreads();
-  stage_slice(slices, 2, ring0, wave, lane);
-  slice256(acc, ring1, enc[1], lane);
-  __syncthreads();
-  bias_act(act, acc, hd + kHeadBias + 0 * 256 + h * 128, true);
-  int g = 2;   // next slice to compute (always even at a layer start)
+  for (int m = 0; m < 16; ++m) acc[m] = f32x4(0.0f);
+  slice256<0>(acc, R.buf(0), enc, lane, R.dma_for(0)); slice_end<2>();
+  slice256<1>(acc, R.buf(1), enc, lane, R.dma_for(1)); slice_end<2>();
+  bias_act(act, acc, hd + kHeadBias + 0 * 256 + g4 * 64, true);
+  int g = 2;   // next slice to compute
 
   float alpha = 0.0f;
   // ---- layers 1..7 (skip input at 5) + feature (8, no ReLU) ----------------
   for (int L = 1; L <= 8; ++L) {
 #pragma unroll
-    for (int m = 0; m < 8; ++m) acc[m] = f32x16(0.0f);
+    for (int m = 0; m < 16; ++m) acc[m] = f32x4(0.0f);
     if (L == 5) {   // cat(input_pts, h): the encoded input first (NET:57-58)
-      stage_slice(slices, g + 1, ring1, wave, lane);
-      slice256(acc, ring0, enc[0], lane);
-      __syncthreads();
-      stage_slice(slices, g + 2, ring0, wave, lane);
-      slice256(acc, ring1, enc[1], lane);
-      __syncthreads();
+      slice256<0>(acc, R.buf(g), enc, lane, R.dma_for(g)); slice_end<2>();
+      slice256<1>(acc, R.buf(g + 1), enc, lane, R.dma_for(g + 1)); slice_end<2>();
       g += 2;
     }
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) {
-      stage_slice(slices, g + 1, ring1, wave, lane);
-      slice256(acc, ring0, act[i], lane);
-      __syncthreads();
-      stage_slice(slices, g + 2, ring0, wave, lane);
-      slice256(acc, ring1, act[i + 1], lane);
-      __syncthreads();
-      g += 2;
-    }
-    bias_act(act, acc, hd + kHeadBias + L * 256 + h * 128, L != 8);
-    if (L == 7) {   // density head on h (NET:61): VALU dot + cross-half add
-      const float* aw = hd + kHeadAlphaW + h * 128;
+    layer_body(acc, act, R, g);
+    g += 8;
+    bias_act(act, acc, hd + kHeadBias + L * 256 + g4 * 64, L != 8);
+    if (L == 7) {   // density head on h (NET:61): VALU dot + lane-group butterfly
+      const float* aw = hd + kHeadAlphaW + g4 * 64;
       float part = 0.0f;
 #pragma unroll
-      for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < 16; ++m)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) part = __builtin_fmaf(act[m][r], aw[16 * m + r], part);
-      alpha = (part + __shfl_xor(part, 32)) + hd[kHeadAlphaB];
+        for (int r = 0; r < 4; ++r) part = __builtin_fmaf(act[m][r], aw[4 * m + r], part);
+      alpha = quad_sum(part) + hd[kHeadAlphaB];
     }
   }
 
   // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67) -
-  f32x16 acc4[4];
+  // slices 68..72; the counted waits shrink as the ring runs dry
+  f32x4 acc8[8];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc4[m] = f32x16(0.0f);
-#pragma unroll
-  for (int i = 0; i < 4; i += 2) {
-    stage_slice(slices, g + 1, ring1, wave, lane);
-    slice128<8>(acc4, ring0, act[2 * i], act[2 * i + 1], lane);
-    __syncthreads();
-    stage_slice(slices, g + 2, ring0, wave, lane);
-    slice128<8>(acc4, ring1, act[2 * i + 2], act[2 * i + 3], lane);
-    __syncthreads();
-    g += 2;
-  }
-  f32x16 dir[1];
-  encode<4, 1>(dv, h, dir);
-  slice128<4>(acc4, ring0, dir[0], dir[0], lane);
+  for (int m = 0; m < 8; ++m) acc8[m] = f32x4(0.0f);
+  slice128<4, 0>(acc8, R.buf(g), act, lane, R.dma_for(g)); slice_end<2>();           // 68
+  slice128<4, 4>(acc8, R.buf(g + 1), act, lane, R.dma_for(g + 1)); slice_end<2>();   // 69
+  slice128<4, 8>(acc8, R.buf(g + 2), act, lane, R.dma_for(g + 2)); slice_end<1>();   // 70
+  slice128<4, 12>(acc8, R.buf(g + 3), act, lane, R.dma_for(g + 3)); slice_end<0>();  // 71
+  f32x4 dir[2];
+  encode<4, 2>(dv, g4, dir);
+  slice128<2, 0>(acc8, R.buf(g + 4), dir, lane, R.dma_for(g + 4));                   // 72
 
   // ---- rgb head (NET:68-70) on the VALU ------------------------------------
-  const float* bvw = hd + kHeadBiasViews + h * 64;
+  const float* bvw = hd + kHeadBiasViews + g4 * 32;
   float part[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
+  for (int m = 0; m < 8; ++m) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = fmaxf(acc4[m][r] + bvw[16 * m + r], 0.0f);
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(acc8[m][r] + bvw[4 * m + r], 0.0f);
 #pragma unroll
       for (int c = 0; c < 3; ++c)
-        part[c] = __builtin_fmaf(v, hd[kHeadRgbW + c * 128 + h * 64 + 16 * m + r], part[c]);
+        part[c] = __builtin_fmaf(v, hd[kHeadRgbW + c * 128 + g4 * 32 + 4 * m + r], part[c]);
     }
   }
   float rgb[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) rgb[c] = (part[c] + __shfl_xor(part[c], 32)) + hd[kHeadRgbB + c];
-  if (valid && h == 0) raw[gs] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
+  for (int c = 0; c < 3; ++c) rgb[c] = quad_sum(part[c]) + hd[kHeadRgbB + c];
+  if (valid && g4 == 0) raw[gs] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
 }
 
 }  // namespace nerfhip

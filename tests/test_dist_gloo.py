@@ -1,0 +1,78 @@
+"""Row-band / chunk-aligned frame sharding + the pixel all-gather (nerfhip.dist),
+world_size 2 over gloo on the CPU. The per-band render is a deterministic
+function of the pixel index, so the assembled frame must equal the
+single-process frame exactly."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from nerfhip import dist as nd
+
+
+def fake_render(p0, n, with_fine=True):
+    p = torch.arange(p0, p0 + n, dtype=torch.float32)
+    out = {"rgb_map_0": torch.stack([p, p + 0.25, p + 0.5], -1), "disp_map_0": -p,
+           "acc_map_0": p * 0.5, "depth_map_0": p + 3.0}
+    if with_fine:
+        out.update({"rgb_map": torch.stack([2 * p, 2 * p + 1, 2 * p + 2], -1), "disp_map": p * 3,
+                    "acc_map": p - 1, "depth_map": p * 7})
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, H, W, chunk_aligned, with_fine, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frame = nd.render_frame_sharded(lambda p0, n: fake_render(p0, n, with_fine), H, W, rank,
+                                        world, torch.device("cpu"), chunk_aligned=chunk_aligned)
+        q.put((rank, {k: v.clone() for k, v in frame.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H,W,chunk_aligned,with_fine", [(8, 5, False, True), (7, 3, False, True),
+                                                         (64, 80, True, True), (3, 1000, True, False)])
+def test_two_rank_frame_equals_single(H, W, chunk_aligned, with_fine):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, H, W, chunk_aligned, with_fine, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = fake_render(0, H * W, with_fine)
+    for rank in (0, 1):
+        frame = got[rank]
+        assert set(frame) == set(ref)
+        for k, v in ref.items():
+            shape = (H, W, 3) if k.startswith("rgb") else (H, W)
+            assert torch.equal(frame[k], v.reshape(shape)), (rank, k)
+
+
+def test_band_partition_covers_image():
+    for H, W, world in [(800, 800, 8), (800, 800, 3), (5, 7, 8)]:
+        for aligned in (False, True):
+            seen = []
+            for r in range(world):
+                p0, n, pad = nd.band(H, W, r, world, aligned)
+                assert n <= pad
+                if aligned and p0 < H * W:
+                    assert p0 % nd.REF_CHUNK == 0
+                seen.extend(range(p0, p0 + n))
+            assert seen == list(range(H * W))

@@ -1,0 +1,82 @@
+"""Timing-only A/B of MLP kernel variants, interleaved in one process.
+
+    python tools/mlp_ablate.py build            # CPU: builds build/abl/lib_<v>.so
+    python tools/mlp_ablate.py run [rounds]     # GPU: times each variant
+
+Variants are compile-time switches in csrc/mlp_fused.hip (ABL_*). Outputs of
+ablated variants are wrong by construction; only their time is meaningful.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "nerf-rep_for_test_amd")
+OUT = os.path.join(PKG, "build", "abl")
+VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
+            "nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"], "noenc": ["-DABL_NOENC"],
+            "noepi": ["-DABL_NOEPI"]}
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-shared"]
+
+
+def build(names):
+    os.makedirs(OUT, exist_ok=True)
+    for v in names:
+        cmd = ["/opt/rocm/bin/hipcc", *FLAGS, *VARIANTS[v], os.path.join(PKG, "csrc", "runtime.hip"),
+               os.path.join(PKG, "csrc", "mlp_fused.hip"), "-o", os.path.join(OUT, f"lib_{v}.so")]
+        subprocess.check_call(cmd)
+        print("built", v)
+
+
+def run(names, rounds, n_rays, S):
+    sys.path.insert(0, PKG)
+    import numpy as np
+    import torch
+    from nerfhip.pack import pack_mlp
+    from nerfhip.synthetic import make_params
+    dev = torch.device("cuda:0")
+    sl, hd = pack_mlp(make_params(0, 2.0, 0.0), "model")
+    sl, hd = torch.from_numpy(sl).to(dev), torch.from_numpy(hd).to(dev)
+    g = torch.Generator().manual_seed(0)
+    ro = (torch.rand((n_rays, 3), generator=g) * 0.2 + torch.tensor([0.0, 2.7, 3.0])).to(dev)
+    rd = torch.nn.functional.normalize(torch.randn((n_rays, 3), generator=g), dim=1).to(dev)
+    z = torch.linspace(2.0, 6.0, S).to(dev)
+    raw = torch.empty((n_rays * S, 4), device=dev)
+    libs = {}
+    for v in names:
+        h = ctypes.CDLL(os.path.join(OUT, f"lib_{v}.so"))
+        h.nerf_mlp_forward.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int64,
+                                                               ctypes.c_int, ctypes.c_void_p,
+                                                               ctypes.c_void_p]
+        libs[v] = h
+    stream = torch.cuda.current_stream().cuda_stream
+    times = {v: [] for v in names}
+    for r in range(rounds + 1):
+        for v in names:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = libs[v].nerf_mlp_forward(sl.data_ptr(), hd.data_ptr(), ro.data_ptr(), rd.data_ptr(),
+                                          z.data_ptr(), 0, n_rays, S, raw.data_ptr(), stream)
+            e1.record()
+            assert rc == 0, (v, rc)
+            torch.cuda.synchronize()
+            if r > 0:
+                times[v].append(e0.elapsed_time(e1))
+    flops = n_rays * S * 1186816
+    for v in names:
+        t = sorted(times[v])
+        med = t[len(t) // 2]
+        print(f"{v:14s} median {med:8.2f} ms  min {t[0]:8.2f}  TF {flops / med / 1e9:7.1f}  "
+              f"frac {flops / med / 1e9 / 157.3:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    names = [v for v in VARIANTS if v in (sys.argv[3:] or VARIANTS)]
+    if sys.argv[1] == "build":
+        build(names)
+    else:
+        names = [v for v in names if os.path.exists(os.path.join(OUT, f"lib_{v}.so"))]
+        run(names, int(sys.argv[2]) if len(sys.argv) > 2 else 5, 160000, 64)
