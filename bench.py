@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--H", type=int, default=800)
     ap.add_argument("--W", type=int, default=800)
-    ap.add_argument("--cpu-rows", type=int, default=8,
+    ap.add_argument("--cpu-rows", type=int, default=24,
                     help="rows of the frame the CPU oracle baseline renders")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -101,9 +101,10 @@ def main():
         elapsed = float(t.item())
 
     # dominant kernel: the fused MLP (coarse + fine launches), HIP events on its stream
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _ in pipe.timer)
-    mlp_samples = sum(s for _, _, s in pipe.timer)
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _, _ in pipe.timer)
+    mlp_samples = sum(s for _, _, s, _ in pipe.timer)
     n_launch = len(pipe.timer)
+    mlp_bytes = sum(b for _, _, _, b in pipe.timer)   # NerfPipeline.mlp_bytes per launch
     pipe.timer = None
     flops = mlp_samples * NerfPipeline.MLP_FLOP_PER_SAMPLE
     achieved = flops / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
@@ -128,7 +129,10 @@ def main():
                    "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
         "roofline": {"bound": "mfma", "kernel": "mlp_fused_kernel",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": pmc_traffic(H, W),
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+                     "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
                      "launches": n_launch,
                      "avg_launch_ms": mlp_ms / max(1, n_launch),
                      "flop_per_sample": NerfPipeline.MLP_FLOP_PER_SAMPLE,
@@ -142,6 +146,21 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(H, W):
+    """Measured HBM bytes per MLP launch from the newest committed PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py) taken on this same workload, else None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json"))):
+        with open(f) as fh:
+            doc = json.load(fh)
+        wl = doc.get("workload", {})
+        e = doc.get("kernels", {}).get("mlp_fused", {})
+        if wl.get("H") == H and wl.get("W") == W and "hbm_bytes_per_launch" in e:
+            best = e["hbm_bytes_per_launch"]
+    return best
 
 
 def cpu_baseline(pipe, H, W, params, rows):

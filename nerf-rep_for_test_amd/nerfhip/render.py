@@ -61,7 +61,7 @@ class NerfPipeline:
         self.grid_res = 0
         self.coarse = None
         self.fine = None
-        self.timer = None         # list -> (start event, end event, samples) per MLP launch
+        self.timer = None         # list -> (start event, end event, samples, bytes) per MLP launch
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, params, coarse_prefix="model", fine_prefix="model_fine"):
@@ -81,6 +81,13 @@ class NerfPipeline:
     # algorithmic MACs of one NeRF MLP evaluation (NET:49-74): 63*256 + 4*256^2
     # + 319*256 + 2*256^2 + 256 (alpha) + 256^2 (feature) + 283*128 + 128*3
     MLP_FLOP_PER_SAMPLE = 2 * 593408
+    MLP_WEIGHT_BYTES = 4 * (_lib.MLP_SLICES * _lib.MLP_SLICE_FLOATS + _lib.MLP_HEAD_FLOATS)
+
+    @classmethod
+    def mlp_bytes(cls, n, S, z_stride):
+        """Algorithmic HBM bytes of one MLP launch: raw out (16 B/sample), rays o/d
+        (24 B/ray), z (4 B/sample, or one shared row when z_stride == 0), weights once."""
+        return n * S * 16 + n * 24 + (n * S if z_stride else S) * 4 + cls.MLP_WEIGHT_BYTES
 
     def mlp(self, packed, rays_o, rays_d, z, z_stride, n, S):
         raw = torch.empty((n * S, 4), device=self.device, dtype=torch.float32)
@@ -93,7 +100,7 @@ class NerfPipeline:
              ptr(z), z_stride, n, S, ptr(raw), _lib.stream_of(self.device))
         if t is not None:
             e1.record()
-            t.append((e0, e1, n * S))
+            t.append((e0, e1, n * S, self.mlp_bytes(n, S, z_stride)))
         return raw
 
     def composite(self, raw, z, z_stride, rays_d, n, S, out, off):

@@ -8,10 +8,11 @@ mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --H 256 --W 256}
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 i=0
-for grp in ${PMC_GROUPS:-"FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY"}; do
+for grp in ${PMC_GROUPS:-FETCH_SIZE WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES__GRBM_GUI_ACTIVE__SQ_WAVE_CYCLES__SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT__SQ_INSTS_LDS__SQ_INSTS_VALU_MFMA_F32}; do
   i=$((i+1))
   echo "== pass $i: $grp"
-  timeout -k 10 600 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o pmc \
+  # a group is counters joined by "__" (one env word); rocprofv3 takes them space-separated
+  timeout -k 10 600 rocprofv3 --pmc ${grp//__/ } --kernel-trace --output-format csv -d "$OUT/p$i" -o pmc \
       -- python bench.py $ARGS > "$OUT/p$i.log" 2>&1
   rc=$?; echo "rc=$rc"; tail -2 "$OUT/p$i.log"
   if [ $rc -ne 0 ]; then echo "STOP"; exit $rc; fi
