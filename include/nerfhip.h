@@ -91,7 +91,8 @@ int nerf_composite_ert(const float* raw, const float* z, int64_t z_stride,
 
 /* VR:239-268 + VR:181-183: inverse-CDF fine sampling from the coarse weights
  * and merge: z_all[n][S+n_imp] = sort(concat(z, samples)).
- * u: [n_imp] (u_stride 0, eval) or [n][n_imp] (training draws). */
+ * u: [n_imp] (u_stride 0, eval) or [n][n_imp] (training draws).
+ * Limits: 3 <= S <= 130 coarse samples, 1 <= n_imp <= 256. */
 int nerf_sample_fine(const float* z, int64_t z_stride, const float* weights,
                      const float* u, int64_t u_stride, int64_t n, int S, int n_imp,
                      float* z_all, nerf_stream_t stream);

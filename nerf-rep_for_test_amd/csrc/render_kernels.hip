@@ -61,188 +61,309 @@ __global__ void coarse_kernel(const float* __restrict__ z_base, const float* __r
 }
 
 // ---------------------------------------------------------------------------
-// compositing (VR:286-357) — one thread per ray
+// compositing (VR:286-357) — one wave per ray, lanes over samples
+//
+// Per 64-sample block: one coalesced float4 raw load + z[s], z[s+1] per lane,
+// alpha, an in-wave double-precision product scan for the transmittance
+// (torch's CPU cumprod accumulates float in double, VR:329), w = alpha * T.
+// The map sums are wave reductions (a different addition order than torch's
+// CPU sum: differences are at the 1e-7 level, well inside the 1e-5 contract;
+// the weights themselves, which feed _sample_fine, are elementwise).
 // ---------------------------------------------------------------------------
-struct RaySpan {
-  const float4* raw;   // [S] (rgb logits, sigma)
-  const float* z;      // [S]
-  float nd;            // torch.norm(rays_d) of the (already unit) direction
-};
-
-__device__ __forceinline__ float dist_at(const RaySpan& r, int S, int s) {
-  const float d = (s < S - 1) ? (r.z[s + 1] - r.z[s]) : 1e10f;
-  return d * r.nd;
-}
-
-__device__ __forceinline__ float alpha_at(const RaySpan& r, int S, int s) {
-  const float sig = fmaxf(r.raw[s].w, 0.0f);                   // relu (raw + noise 0)
-  return 1.0f - expf((-sig) * dist_at(r, S, s));               // VR:288
-}
-
 __device__ __forceinline__ float sigmoid_t(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__device__ void write_maps(const RaySpan& r, int S, const float* w, int64_t ray, int white,
-                           float* rgb, float* disp, float* acc, float* depth) {
-  float c[3];
-#pragma unroll
-  for (int ch = 0; ch < 3; ++ch) {
-    c[ch] = tsum_dim2(S, [&](int s) {
-      const float4 v = r.raw[s];
-      const float x = ch == 0 ? v.x : (ch == 1 ? v.y : v.z);
-      return w[s] * sigmoid_t(x);
-    });
-  }
-  const float dep = tsum_last(S, [&](int s) { return w[s] * r.z[s]; });
-  const float ac = tsum_last(S, [&](int s) { return w[s]; });
-  const float ratio = dep / ac;
-  disp[ray] = 1.0f / torch_max(1e-10f, ratio);
-  acc[ray] = ac;
-  depth[ray] = dep;
-#pragma unroll
-  for (int ch = 0; ch < 3; ++ch) rgb[ray * 3 + ch] = white ? c[ch] + (1.0f - ac) : c[ch];
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
 }
 
-__global__ void composite_kernel(const float4* __restrict__ raw, const float* __restrict__ z,
-                                 int64_t z_stride, const float* __restrict__ rays_d, int64_t n,
-                                 int S, int white, float* __restrict__ rgb,
-                                 float* __restrict__ disp, float* __restrict__ acc,
-                                 float* __restrict__ depth, float* __restrict__ wout) {
-  const int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ray >= n) return;
-  RaySpan r;
-  r.raw = raw + ray * S;
-  r.z = z + ray * z_stride;
-  r.nd = torch_norm3(rays_d[ray * 3], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]);
-  float* w = wout + ray * S;
-  // w_s = alpha_s * cumprod([1, 1-alpha+1e-10])_s, scan accumulated in double (VR:329)
-  double T = 1.0;
-  for (int s = 0; s < S; ++s) {
-    const float a = alpha_at(r, S, s);
-    w[s] = a * (float)T;
-    T = T * (double)((1.0f - a) + 1e-10f);
+__device__ __forceinline__ double wave_prod_scan(double p, int lane) {   // inclusive
+  for (int o = 1; o < 64; o <<= 1) {
+    const double q = __shfl_up(p, o);
+    if (lane >= o) p *= q;
   }
-  write_maps(r, S, w, ray, white, rgb, disp, acc, depth);
+  return p;
 }
 
-// ERT (VR:1089-1133): T = cumprod(1 - [0, alpha[:-1]]) without the 1e-10; if
-// any ray of the 2048-ray chunk has T < thr, every ray's weights are cut from
-// argmax(T < thr) on (0 for rays that never cross it). One block per chunk.
-__global__ void composite_ert_kernel(const float4* __restrict__ raw, const float* __restrict__ z,
-                                     int64_t z_stride, const float* __restrict__ rays_d,
-                                     int64_t n, int S, int white, float thr, int chunk,
-                                     float* __restrict__ rgb, float* __restrict__ disp,
-                                     float* __restrict__ acc, float* __restrict__ depth,
-                                     float* __restrict__ wout) {
+struct Maps {
+  float r, g, b, d, a;   // sum w*rgb, sum w*z, sum w
+};
+
+__device__ __forceinline__ void maps_add(Maps& m, float w, const float4& v, float z) {
+  m.r += w * sigmoid_t(v.x);
+  m.g += w * sigmoid_t(v.y);
+  m.b += w * sigmoid_t(v.z);
+  m.d += w * z;
+  m.a += w;
+}
+
+__device__ __forceinline__ Maps maps_reduce(Maps m) {
+  return Maps{wave_sum(m.r), wave_sum(m.g), wave_sum(m.b), wave_sum(m.d), wave_sum(m.a)};
+}
+
+// VR:331-334, 353-354: disp = 1/max(1e-10, depth/acc), white background.
+__device__ __forceinline__ void maps_store(const Maps& m, int64_t ray, int white, float* rgb,
+                                           float* disp, float* acc, float* depth) {
+  disp[ray] = 1.0f / torch_max(1e-10f, m.d / m.a);
+  acc[ray] = m.a;
+  depth[ray] = m.d;
+  const float bg = white ? 1.0f - m.a : 0.0f;
+  rgb[ray * 3 + 0] = white ? m.r + bg : m.r;
+  rgb[ray * 3 + 1] = white ? m.g + bg : m.g;
+  rgb[ray * 3 + 2] = white ? m.b + bg : m.b;
+}
+
+// One ray by one wave. ERT: T without the +1e-10 (VR:1109-1111); `first` = the
+// first s with T_s < thr or -1, and `cut` = the sums with w[first:] * 0
+// (VR:1115-1123), valid when first >= 0.
+template <bool ERT>
+__device__ __forceinline__ void composite_ray(const float4* __restrict__ rr,
+                                              const float* __restrict__ zr, float nd, int S,
+                                              int lane, float thr, float* __restrict__ w_out,
+                                              Maps& full, Maps& cut, int& first) {
+  full = Maps{0, 0, 0, 0, 0};
+  cut = Maps{0, 0, 0, 0, 0};
+  first = -1;
+  double carry = 1.0;
+  for (int b = 0; b < S; b += 64) {
+    const int s = b + lane;
+    const bool act = s < S;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    float zs = 0.f, a = 0.f;
+    if (act) {
+      v = rr[s];
+      zs = zr[s];
+      const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;   // VR:290-292
+      a = 1.0f - expf((-fmaxf(v.w, 0.0f)) * dist);                       // VR:288
+    }
+    const double f = act ? (double)(ERT ? (1.0f - a) : ((1.0f - a) + 1e-10f)) : 1.0;
+    const double inc = wave_prod_scan(f, lane);
+    double ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = 1.0;
+    const float T = (float)(carry * ex);
+    carry = carry * __shfl(inc, 63);
+    const float w = a * T;
+    if (act) {
+      if (w_out) w_out[s] = w;
+      maps_add(full, w, v, zs);
+    }
+    if constexpr (ERT) {
+      const uint64_t low = __ballot(act && T < thr);
+      if (first < 0 && low) first = b + (int)__builtin_ctzll(low);
+      if (act) maps_add(cut, (first < 0 || s < first) ? w : w * 0.0f, v, zs);
+    }
+  }
+  full = maps_reduce(full);
+  if constexpr (ERT) cut = maps_reduce(cut);
+}
+
+constexpr int COMP_WAVES = 4;
+
+__global__ __launch_bounds__(64 * COMP_WAVES) void composite_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
+    const float* __restrict__ rays_d, int64_t n, int S, int white, float* __restrict__ rgb,
+    float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ depth,
+    float* __restrict__ wout) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ray = (int64_t)blockIdx.x * COMP_WAVES + (threadIdx.x >> 6);
+  if (ray >= n) return;   // wave-uniform
+  const float nd = torch_norm3(rays_d[ray * 3], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]);
+  Maps full, cut;
+  int first;
+  composite_ray<false>(raw + ray * S, z + ray * z_stride, nd, S, lane, 0.f,
+                       wout ? wout + ray * S : nullptr, full, cut, first);
+  if (lane == 0) maps_store(full, ray, white, rgb, disp, acc, depth);
+}
+
+// ERT (VR:1089-1133): if any ray of the 2048-ray chunk has T < thr, every ray's
+// weights are cut from argmax(T < thr) on (0 for rays that never cross it, so
+// they composite to nothing). One block per chunk: the uncut maps go straight
+// to the outputs, the cut ones wait in LDS for the chunk-wide decision.
+constexpr int ERT_WAVES = 8;
+constexpr int ERT_MAX_CHUNK = 2048;
+
+__global__ __launch_bounds__(64 * ERT_WAVES) void composite_ert_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
+    const float* __restrict__ rays_d, int64_t n, int S, int white, float thr, int chunk,
+    float* __restrict__ rgb, float* __restrict__ disp, float* __restrict__ acc,
+    float* __restrict__ depth, float* __restrict__ wout) {
+  __shared__ Maps cut_s[ERT_MAX_CHUNK];
+  __shared__ int first_s[ERT_MAX_CHUNK];
   __shared__ int any_low;
   if (threadIdx.x == 0) any_low = 0;
   __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * chunk;
-  const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
-  // pass 1: weights without the cut + first termination index per ray
-  for (int64_t ray = c0 + threadIdx.x; ray < c1; ray += blockDim.x) {
-    RaySpan r;
-    r.raw = raw + ray * S;
-    r.z = z + ray * z_stride;
-    r.nd = torch_norm3(rays_d[ray * 3], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]);
-    float* w = wout + ray * S;
-    double T = 1.0;
-    int first = -1;
-    for (int s = 0; s < S; ++s) {
-      const float a = alpha_at(r, S, s);
-      const float Tf = (float)T;
-      if (first < 0 && Tf < thr) first = s;
-      w[s] = a * Tf;
-      T = T * (double)(1.0f - a);
+  const int nr = (int)((c0 + chunk < n ? c0 + chunk : n) - c0);
+  for (int i = wave; i < nr; i += ERT_WAVES) {
+    const int64_t ray = c0 + i;
+    const float nd = torch_norm3(rays_d[ray * 3], rays_d[ray * 3 + 1], rays_d[ray * 3 + 2]);
+    Maps full, cut;
+    int first;
+    composite_ray<true>(raw + ray * S, z + ray * z_stride, nd, S, lane, thr,
+                        wout ? wout + ray * S : nullptr, full, cut, first);
+    if (lane == 0) {
+      maps_store(full, ray, white, rgb, disp, acc, depth);
+      cut_s[i] = first >= 0 ? cut : Maps{0, 0, 0, 0, 0};
+      first_s[i] = first >= 0 ? first : 0;          // argmax of an all-False row
+      if (first >= 0) any_low = 1;                 // benign race: every writer stores 1
     }
-    if (first >= 0) any_low = 1;   // benign race: every writer stores 1
-    // stash the termination index in the (otherwise unused) depth slot
-    depth[ray] = __int_as_float(first);
   }
   __syncthreads();
-  const bool cut = any_low != 0;
-  for (int64_t ray = c0 + threadIdx.x; ray < c1; ray += blockDim.x) {
-    RaySpan r;
-    r.raw = raw + ray * S;
-    r.z = z + ray * z_stride;
-    r.nd = 0.f;
-    float* w = wout + ray * S;
-    if (cut) {
-      int first = __float_as_int(depth[ray]);
-      if (first < 0) first = 0;        // argmax of an all-False row
-      for (int s = first; s < S; ++s) w[s] = w[s] * 0.0f;
-    }
-    write_maps(r, S, w, ray, white, rgb, disp, acc, depth);
+  if (!any_low) return;
+  for (int i = wave; i < nr; i += ERT_WAVES) {
+    const int64_t ray = c0 + i;
+    const int f0 = first_s[i];
+    if (lane == 0) maps_store(cut_s[i], ray, white, rgb, disp, acc, depth);
+    if (wout)
+      for (int s = f0 + lane; s < S; s += 64) wout[ray * S + s] = wout[ray * S + s] * 0.0f;
   }
 }
 
 // ---------------------------------------------------------------------------
 // fine sampling (VR:239-268) + merge with the coarse depths (VR:181-183)
-// one thread per ray; cdf and bins staged in LDS as [index][thread]
+// one wave per ray, 4 rays per block; per-wave LDS rows
 // ---------------------------------------------------------------------------
-constexpr int FINE_BLOCK = 64;
-constexpr int FINE_MAX_NB = 128;   // S <= 129 coarse samples
+constexpr int FINE_WAVES = 4;
+constexpr int FINE_MAX_S = 130;      // coarse samples per ray
+constexpr int FINE_MAX_IMP = 256;    // fine samples per ray
+constexpr int FINE_ROW = FINE_MAX_S + 2;
 
-__global__ __launch_bounds__(FINE_BLOCK) void sample_fine_kernel(
+struct FineLds {
+  float zc[FINE_ROW];        // coarse depths (sorted)
+  float wv[FINE_ROW];        // weights[1:-1] + 1e-5
+  float cdf[FINE_ROW];       // [0, cumsum(pdf)]
+  float bins[FINE_ROW];      // mids of z
+  float zf[FINE_MAX_IMP];    // fine samples, sorted in place
+};
+
+// torch.sum(x, -1) in ATen's order (common.h tsum_last), computed by the whole
+// wave: lane l < 8 folds vector lane l's four accumulators, the scalar tail and
+// the final in-order combination are evaluated redundantly by every lane.
+__device__ __forceinline__ float wave_tsum_last(const float* v, int n, int lane) {
+  if (n < 8) return tsum_last(n, [&](int i) { return v[i]; });
+  const int nv = n >> 3, nilp = nv >> 2, l = lane & 7;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int ii = 0; ii < nilp; ++ii) {
+    const int b = ii * 32 + l;
+    a0 = a0 + v[b];
+    a1 = a1 + v[b + 8];
+    a2 = a2 + v[b + 16];
+    a3 = a3 + v[b + 24];
+  }
+  for (int q = nilp * 4; q < nv; ++q) a0 = a0 + v[q * 8 + l];
+  const float part = ((a0 + a1) + a2) + a3;
+  float fin = 0.f;
+  for (int k = nv * 8; k < n; ++k) fin = fin + v[k];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) fin = fin + __shfl(part, q);
+  return fin;
+}
+
+__device__ __forceinline__ double wave_sum_scan(double p, int lane) {   // inclusive
+  for (int o = 1; o < 64; o <<= 1) {
+    const double q = __shfl_up(p, o);
+    if (lane >= o) p += q;
+  }
+  return p;
+}
+
+// number of a[0..n) < x  (a ascending)
+__device__ __forceinline__ int lower_bound(const float* a, int n, float x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+// number of a[0..n) <= x
+__device__ __forceinline__ int upper_bound(const float* a, int n, float x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
     const float* __restrict__ z, int64_t z_stride, const float* __restrict__ weights,
     const float* __restrict__ u, int64_t u_stride, int64_t n, int S, int n_imp,
     float* __restrict__ z_all) {
-  __shared__ float cdf_s[FINE_MAX_NB * FINE_BLOCK];
-  __shared__ float bin_s[FINE_MAX_NB * FINE_BLOCK];
-  const int t = threadIdx.x;
-  const int64_t ray = (int64_t)blockIdx.x * FINE_BLOCK + t;
-  if (ray >= n) return;
+  __shared__ FineLds sm[FINE_WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t ray = (int64_t)blockIdx.x * FINE_WAVES + wave;
+  if (ray >= n) return;   // wave-uniform; no block barriers below
+  FineLds& L = sm[wave];
   const float* zr = z + ray * z_stride;
   const float* wr = weights + ray * S;
-  const int nb = S - 1;       // bins = mids of z (63), cdf has nb entries
+  const int nb = S - 1;       // bins = mids of z; the cdf has nb entries
   const int nw = S - 2;       // weights[..., 1:-1]
-  // pdf normaliser: torch.sum(weights + 1e-5, -1)
-  const float tot = tsum_last(nw, [&](int s) { return wr[s + 1] + 1e-5f; });
-  double run = 0.0;
-  cdf_s[t] = 0.0f;
-  for (int s = 0; s < nw; ++s) {
-    const float pdf = (wr[s + 1] + 1e-5f) / tot;
-    run += (double)pdf;
-    cdf_s[(s + 1) * FINE_BLOCK + t] = (float)run;
+  for (int s = lane; s < S; s += 64) L.zc[s] = zr[s];
+  for (int s = lane; s < nw; s += 64) L.wv[s] = wr[s + 1] + 1e-5f;
+  __builtin_amdgcn_wave_barrier();
+  for (int s = lane; s < nb; s += 64) L.bins[s] = 0.5f * (L.zc[s + 1] + L.zc[s]);
+  // pdf = w / torch.sum(w, -1); cdf = [0, cumsum(pdf)] accumulated in double
+  const float tot = wave_tsum_last(L.wv, nw, lane);
+  double carry = 0.0;
+  if (lane == 0) L.cdf[0] = 0.0f;
+  for (int b = 0; b < nw; b += 64) {
+    const int s = b + lane;
+    const double pdf = s < nw ? (double)(L.wv[s] / tot) : 0.0;
+    const double inc = carry + wave_sum_scan(pdf, lane);
+    if (s < nw) L.cdf[s + 1] = (float)inc;
+    carry = __shfl(inc, 63);
   }
-  for (int s = 0; s < nb; ++s) bin_s[s * FINE_BLOCK + t] = 0.5f * (zr[s + 1] + zr[s]);
-  // fine samples are staged in the tail of this ray's output row
-  float* out = z_all + ray * (int64_t)(S + n_imp);
-  float* zf = out + S;
+  __builtin_amdgcn_wave_barrier();
+  // inverse CDF (searchsorted right=True, clamp, lerp; VR:254-266)
   const float* ur = u + ray * u_stride;
-  for (int j = 0; j < n_imp; ++j) {
-    const float uj = ur[j];
-    // searchsorted(cdf, u, right=True): number of cdf entries <= u
-    int lo = 0, hi = nb;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (cdf_s[mid * FINE_BLOCK + t] <= uj) lo = mid + 1; else hi = mid;
+  int p2 = 64;
+  while (p2 < n_imp) p2 <<= 1;
+  for (int j = lane; j < p2; j += 64) {
+    float v = __builtin_inff();
+    if (j < n_imp) {
+      const float uj = ur[j];
+      const int inds = upper_bound(L.cdf, nb, uj);
+      const int below = inds - 1 > 0 ? inds - 1 : 0;
+      const int above = inds < nb - 1 ? inds : nb - 1;
+      const float cg0 = L.cdf[below], cg1 = L.cdf[above];
+      const float bg0 = L.bins[below], bg1 = L.bins[above];
+      float denom = cg1 - cg0;
+      denom = denom < 1e-5f ? 1.0f : denom;
+      const float t = (uj - cg0) / denom;
+      v = bg0 + t * (bg1 - bg0);
     }
-    const int below = lo - 1 > 0 ? lo - 1 : 0;
-    const int above = lo < nb - 1 ? lo : nb - 1;
-    const float cg0 = cdf_s[below * FINE_BLOCK + t], cg1 = cdf_s[above * FINE_BLOCK + t];
-    const float bg0 = bin_s[below * FINE_BLOCK + t], bg1 = bin_s[above * FINE_BLOCK + t];
-    float denom = cg1 - cg0;
-    denom = denom < 1e-5f ? 1.0f : denom;
-    const float tt = (uj - cg0) / denom;
-    zf[j] = bg0 + tt * (bg1 - bg0);
+    L.zf[j] = v;
   }
-  // torch.sort(cat(z, zf)) (values only): insertion-sort zf (already ascending
-  // in eval mode), then merge it with the ascending coarse row front to back,
-  // in place: while coarse values remain (a < S) the write index a+b stays
-  // below the first unread fine sample at S+b; once they are exhausted the
-  // remaining fine samples already sit at their final positions.
-  for (int j = 1; j < n_imp; ++j) {
-    const float v = zf[j];
-    int k = j - 1;
-    while (k >= 0 && zf[k] > v) { zf[k + 1] = zf[k]; --k; }
-    zf[k + 1] = v;
+  __builtin_amdgcn_wave_barrier();
+  // ascending bitonic sort of the (inf-padded) fine samples
+  for (int k = 2; k <= p2; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = lane; i < p2; i += 64) {
+        const int prt = i ^ jj;
+        if (prt > i) {
+          const float x = L.zf[i], y = L.zf[prt];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { L.zf[i] = y; L.zf[prt] = x; }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
   }
-  int a = 0, b = 0;
-  while (a < S && b < n_imp) {
-    const float za = zr[a], zb = zf[b];
-    if (zb < za) { out[a + b] = zb; ++b; } else { out[a + b] = za; ++a; }
+  // torch.sort(cat(z, z_fine)) values: merge by rank (ties: coarse first; equal
+  // values are interchangeable)
+  float* out = z_all + ray * (int64_t)(S + n_imp);
+  for (int i = lane; i < S; i += 64) {
+    const float x = L.zc[i];
+    out[i + lower_bound(L.zf, n_imp, x)] = x;
   }
-  while (a < S) { out[a + b] = zr[a]; ++a; }
+  for (int j = lane; j < n_imp; j += 64) {
+    const float x = L.zf[j];
+    out[j + upper_bound(L.zc, S, x)] = x;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -399,11 +520,11 @@ int nerf_sample_coarse(const float* z_base, const float* t_rand, int64_t n, int 
 int nerf_composite(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
                    int64_t n, int S, int white_bkgd, float* rgb, float* disp, float* acc,
                    float* depth, float* weights, nerf_stream_t stream) {
-  NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth && weights,
-               "nerf_composite: null pointer (weights scratch is required)");
+  NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth,
+               "nerf_composite: null pointer");
   NERF_REQUIRE(n >= 0 && S >= 2 && S < 1024, "nerf_composite: S must be in [2, 1024)");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(composite_kernel, dim3((unsigned)cdiv(n, 128)), dim3(128), 0,
+  hipLaunchKernelGGL(composite_kernel, dim3((unsigned)cdiv(n, COMP_WAVES)), dim3(64 * COMP_WAVES), 0,
                      as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S,
                      white_bkgd, rgb, disp, acc, depth, weights);
   return check_launch("composite_kernel");
@@ -413,11 +534,12 @@ int nerf_composite_ert(const float* raw, const float* z, int64_t z_stride, const
                        int64_t n, int S, int white_bkgd, float threshold, int chunk, float* rgb,
                        float* disp, float* acc, float* depth, float* weights,
                        nerf_stream_t stream) {
-  NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth && weights,
-               "nerf_composite_ert: null pointer (weights scratch is required)");
-  NERF_REQUIRE(n >= 0 && S >= 2 && S < 1024 && chunk > 0, "nerf_composite_ert: bad size");
+  NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth,
+               "nerf_composite_ert: null pointer");
+  NERF_REQUIRE(n >= 0 && S >= 2 && S < 1024 && chunk > 0 && chunk <= ERT_MAX_CHUNK,
+               "nerf_composite_ert: need 2 <= S < 1024 and 0 < chunk <= 2048");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(composite_ert_kernel, dim3((unsigned)cdiv(n, chunk)), dim3(256), 0,
+  hipLaunchKernelGGL(composite_ert_kernel, dim3((unsigned)cdiv(n, chunk)), dim3(64 * ERT_WAVES), 0,
                      as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S,
                      white_bkgd, threshold, chunk, rgb, disp, acc, depth, weights);
   return check_launch("composite_ert_kernel");
@@ -427,10 +549,10 @@ int nerf_sample_fine(const float* z, int64_t z_stride, const float* weights, con
                      int64_t u_stride, int64_t n, int S, int n_imp, float* z_all,
                      nerf_stream_t stream) {
   NERF_REQUIRE(z && weights && u && z_all, "nerf_sample_fine: null pointer");
-  NERF_REQUIRE(n >= 0 && S >= 3 && S - 1 <= FINE_MAX_NB && n_imp >= 1,
-               "nerf_sample_fine: need 3 <= S <= 129 coarse samples and n_imp >= 1");
+  NERF_REQUIRE(n >= 0 && S >= 3 && S <= FINE_MAX_S && n_imp >= 1 && n_imp <= FINE_MAX_IMP,
+               "nerf_sample_fine: need 3 <= S <= 130 coarse and 1 <= n_imp <= 256 fine samples");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(sample_fine_kernel, dim3((unsigned)cdiv(n, FINE_BLOCK)), dim3(FINE_BLOCK), 0,
+  hipLaunchKernelGGL(sample_fine_kernel, dim3((unsigned)cdiv(n, FINE_WAVES)), dim3(64 * FINE_WAVES), 0,
                      as_stream(stream), z, z_stride, weights, u, u_stride, n, S, n_imp, z_all);
   return check_launch("sample_fine_kernel");
 }

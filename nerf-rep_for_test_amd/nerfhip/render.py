@@ -103,9 +103,11 @@ class NerfPipeline:
             t.append((e0, e1, n * S, self.mlp_bytes(n, S, z_stride)))
         return raw
 
-    def composite(self, raw, z, z_stride, rays_d, n, S, out, off):
-        """Writes rgb/disp/acc/depth rows [off, off+n) of `out`; returns weights."""
-        w = torch.empty((n, S), device=self.device, dtype=torch.float32)
+    def composite(self, raw, z, z_stride, rays_d, n, S, out, off, need_weights=True):
+        """Writes rgb/disp/acc/depth rows [off, off+n) of `out`; returns the weights
+        [n, S] (or None when not needed: the kernel then skips writing them)."""
+        w = (torch.empty((n, S), device=self.device, dtype=torch.float32)
+             if need_weights else None)
         rgb, disp, acc, depth = out
         args = (ptr(raw), ptr(z), z_stride, ptr(rays_d), n, S, int(self.white_bkgd))
         tail = (ptr(rgb[off:]), ptr(disp[off:]), ptr(acc[off:]), ptr(depth[off:]), ptr(w),
@@ -168,7 +170,8 @@ class NerfPipeline:
                 call("nerf_sample_fine", ptr(z), zs, ptr(w), ptr(uu), us, m, S, NI, ptr(zall), st)
                 del raw, w
                 raw_f = self.mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
-                w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p)
+                w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p,
+                                     need_weights=self.enable_ert and self.enable_ess)
                 self._grid_updates(1, counter0, rd, zall, S + NI, raw_f, w_f, m, S + NI)
                 del raw_f, w_f, zall
             if self.enable_ert:       # _raw2outputs_with_ert counts its calls (VR:1157)

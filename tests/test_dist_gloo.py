@@ -37,7 +37,7 @@ def _worker(rank, world, port, H, W, chunk_aligned, with_fine, q):
     try:
         frame = nd.render_frame_sharded(lambda p0, n: fake_render(p0, n, with_fine), H, W, rank,
                                         world, torch.device("cpu"), chunk_aligned=chunk_aligned)
-        q.put((rank, {k: v.clone() for k, v in frame.items()}))
+        q.put((rank, {k: v.numpy().copy() for k, v in frame.items()}))  # by value, not fd
     finally:
         dist.destroy_process_group()
 
@@ -62,7 +62,7 @@ def test_two_rank_frame_equals_single(H, W, chunk_aligned, with_fine):
         assert set(frame) == set(ref)
         for k, v in ref.items():
             shape = (H, W, 3) if k.startswith("rgb") else (H, W)
-            assert torch.equal(frame[k], v.reshape(shape)), (rank, k)
+            assert torch.equal(torch.from_numpy(frame[k]), v.reshape(shape)), (rank, k)
 
 
 def test_band_partition_covers_image():

@@ -122,12 +122,31 @@ def test_composite_given_raw(dev, S, dense, white):
     out = pipe.alloc_outputs(n)["coarse"]
     w = pipe.composite(_t(raw, dev), _t(zr, dev), S, _t(rd, dev), n, S, out, 0)
     rgb, disp, acc, wt, depth = O.raw2outputs(raw, zr, rd, white)
-    # same op sequence and summation order; exp may differ by an ulp (SLEEF vs ocml)
+    # same op sequence; the map sums are wave reductions (another addition order)
+    # and exp may differ by an ulp (SLEEF vs ocml)
     assert max_err(w.cpu().numpy(), wt) < 1e-6
     assert max_err(out[0].cpu().numpy(), rgb) < 1e-6
     assert max_err(out[2].cpu().numpy(), acc) < 1e-6
     assert rel_err(out[3].cpu().numpy(), depth) < 1e-6
     assert rel_err(out[1].cpu().numpy(), disp, floor=1e-3) < 1e-5
+
+
+@pytest.mark.parametrize("ert", [False, True])
+def test_composite_without_weights_output(dev, ert):
+    """weights=NULL (fine pass without ESS): identical maps, nothing else written."""
+    rng = np.random.default_rng(11)
+    n, S = 3000, 192
+    raw = _t(_rand_raw(rng, n, S, True), dev)
+    zr = _t(np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32), dev)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd = _t(rd / np.linalg.norm(rd, axis=1, keepdims=True), dev)
+    pipe = _pipe(dev, N_samples=S, N_importance=0, enable_ert=ert, ert_threshold=0.01)
+    a, b = pipe.alloc_outputs(n)["coarse"], pipe.alloc_outputs(n)["coarse"]
+    w = pipe.composite(raw, zr, S, rd, n, S, a, 0)
+    assert pipe.composite(raw, zr, S, rd, n, S, b, 0, need_weights=False) is None
+    assert w is not None
+    for x, y in zip(a, b):
+        assert torch.equal(torch.nan_to_num(x, 7.0), torch.nan_to_num(y, 7.0))
 
 
 def test_composite_ert_chunks(dev):
@@ -174,10 +193,11 @@ def test_sample_fine_given_reference_weights(dev, name):
     assert np.mean(err < 1e-5) >= 0.97
 
 
-def test_sample_fine_training_u(dev):
-    """Training-mode u (unsorted uniform draws, VR:247-249)."""
-    rng = np.random.default_rng(3)
-    n, S, NI = 300, 64, 128
+@pytest.mark.parametrize("S,NI", [(64, 128), (3, 1), (5, 7), (33, 64), (100, 200), (130, 256)])
+def test_sample_fine_training_u(dev, S, NI):
+    """Training-mode u (unsorted uniform draws, VR:247-249), ragged sizes."""
+    rng = np.random.default_rng(3 + S + NI)
+    n = 300
     zc = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
     wc = (rng.random((n, S)) ** 4).astype(np.float32)
     u = rng.random((n, NI)).astype(np.float32)
