@@ -10,10 +10,16 @@ views), split into row bands across the ranks, maps all-gathered over RCCL.
 Inputs (packed weights, z tables) are resident in HBM before timing starts.
 Weights are synthetic (deterministic generator, no checkpoint offline).
 
+The headline run uses the default MLP arithmetic (--precision f16x3: FP32
+operands as 3-term FP16 splits on FP16 MFMA with FP32 accumulation, held to the
+same parity gates as FP32); the same frames are then timed with
+the FP32-MFMA kernel and reported under "fp32_mfma".
+
 Prints one JSON line (rank 0). Also reports the fused MLP kernel's roofline
-(algorithmic FLOPs / its HIP-event-timed launches vs the FP32 MFMA peak) and
-the CPU oracle (numpy restatement of the reference) timed on a bounded strip of
-the same frame, with the GPU-vs-oracle parity on that strip.
+(its HIP-event-timed launches: executed MFMA FLOP/s vs the dense MFMA peak of
+the type it runs on, plus the algorithmic FP32 FLOP/s) and the CPU oracle
+(numpy restatement of the reference) timed on a bounded strip of the same
+frame, with the GPU-vs-oracle parity on that strip.
 """
 import argparse
 import json
@@ -27,6 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak
+FP16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS   # dense FP16/BF16 MFMA (1/16 rule, ~2.5 PF)
 METRIC = "Mrays/s + ms/frame, lego 800x800 (64c+128f); PSNR vs ref"
 
 
@@ -48,6 +55,11 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=24,
                     help="rows of the frame the CPU oracle baseline renders")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
+                    help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
+                         "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
+    ap.add_argument("--no-fp32-run", action="store_true",
+                    help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
     args = ap.parse_args()
 
     import torch
@@ -69,46 +81,43 @@ def main():
 
     H, W = args.H, args.W
     params = make_params(0, 2.0, 0.0)
-    pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0)
-    pipe.set_weights(params)
-    torch.cuda.synchronize()
-
-    def frame(i):
-        pose, K = lego_camera(H, W, i)
-        return render_frame_sharded(
-            lambda p0, n: pipe.render_image(H, W, pose, K, p0=p0, n=n),
-            H, W, rank, world, dev)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for i in range(args.warmup):
-        frame(i)
-    torch.cuda.synchronize()
-    barrier()
-    pipe.timer = []
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        frame(args.warmup + i)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def measure(precision):
+        """warmup + K timed frames (barrier + sync both sides, max over ranks)."""
+        pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
+                            mlp_precision=precision)
+        pipe.set_weights(params)
 
-    # dominant kernel: the fused MLP (coarse + fine launches), HIP events on its stream
-    mlp_ms = sum(a.elapsed_time(b) for a, b, _, _ in pipe.timer)
-    mlp_samples = sum(s for _, _, s, _ in pipe.timer)
-    n_launch = len(pipe.timer)
-    mlp_bytes = sum(b for _, _, _, b in pipe.timer)   # NerfPipeline.mlp_bytes per launch
-    pipe.timer = None
-    flops = mlp_samples * NerfPipeline.MLP_FLOP_PER_SAMPLE
-    achieved = flops / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+        def frame(i):
+            pose, K = lego_camera(H, W, i)
+            return render_frame_sharded(
+                lambda p0, n: pipe.render_image(H, W, pose, K, p0=p0, n=n),
+                H, W, rank, world, dev)
 
+        for i in range(args.warmup):
+            frame(i)
+        torch.cuda.synchronize()
+        barrier()
+        pipe.timer = []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            frame(args.warmup + i)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        timer, pipe.timer = pipe.timer, None
+        return pipe, elapsed, roofline(precision, timer, elapsed, world, H, W)
+
+    pipe, elapsed, roof = measure(args.precision)
     rays = H * W * args.steps
     result = {
         "metric": METRIC,
@@ -121,34 +130,64 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": DTYPES[args.precision],
         "data": "synthetic weights (deterministic generator, seed 0, gain 2), lego test cameras",
         "config": {"workload": "lego 800x800, 64 coarse + 128 fine samples, 1 frame per step "
                                "(test poses cycled), ESS/ERT off, perturb 0, eval",
                    "H": H, "W": W, "N_samples": 64, "N_importance": 128,
+                   "mlp_precision": args.precision,
                    "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
-        "roofline": {"bound": "mfma", "kernel": "mlp_fused_kernel",
-                     "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS,
-                     "traffic": pmc_traffic(H, W),
-                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
-                     "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
-                     "launches": n_launch,
-                     "avg_launch_ms": mlp_ms / max(1, n_launch),
-                     "flop_per_sample": NerfPipeline.MLP_FLOP_PER_SAMPLE,
-                     "mlp_share_of_step": (mlp_ms / world) / (elapsed * 1e3) if world == 1 else None},
+        "roofline": roof,
     }
-
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(pipe, H, W, params, args.cpu_rows)
         result["psnr_vs_ref"] = result["parity"]["psnr_fine_rgb"]
+    del pipe
+    if args.precision != "fp32" and not args.no_fp32_run:
+        _, el32, roof32 = measure("fp32")
+        result["fp32_mfma"] = {"value": rays / el32 / 1e6, "ms_per_step": el32 / args.steps * 1e3,
+                               "dtype": DTYPES["fp32"], "roofline": roof32}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def pmc_traffic(H, W):
+DTYPES = {"fp32": "fp32",
+          "f16x3": "fp32 operands as 3-term fp16 splits on fp16 mfma, fp32 accumulate"}
+
+
+def roofline(precision, timer, elapsed, world, H, W):
+    """Dominant kernel (the fused MLP: coarse + fine launches), timed by HIP events
+    recorded on the stream it is launched on."""
+    from nerfhip.render import NerfPipeline
+    mlp_ms = sum(a.elapsed_time(b) for a, b, _, _ in timer)
+    mlp_samples = sum(s for _, _, s, _ in timer)
+    n_launch = len(timer)
+    mlp_bytes = sum(b for _, _, _, b in timer)   # NerfPipeline.mlp_bytes per launch
+    flops = mlp_samples * NerfPipeline.MLP_FLOP_PER_SAMPLE
+    algo_tflops = flops / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    if precision == "fp32":
+        kernel, achieved, peak, unit = ("mlp_fused_kernel", algo_tflops, FP32_MFMA_PEAK_TFLOPS,
+                                        "TFLOP/s")
+    else:   # 3 FP16 MFMA products per FP32 product, against the dense FP16 MFMA peak
+        kernel, achieved, peak, unit = ("mlp_x3_kernel", 3 * algo_tflops, FP16_MFMA_PEAK_TFLOPS,
+                                        "TFLOP/s (FP16 MFMA, 3 per FP32 product)")
+    return {"bound": "mfma", "kernel": kernel,
+            "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak,
+            "algorithmic_tflops": algo_tflops,
+            "frac_of_fp32_peak": algo_tflops / FP32_MFMA_PEAK_TFLOPS,
+            "traffic": pmc_traffic(H, W, kernel),
+            "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+            "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
+            "launches": n_launch,
+            "avg_launch_ms": mlp_ms / max(1, n_launch),
+            "flop_per_sample": NerfPipeline.MLP_FLOP_PER_SAMPLE,
+            "mlp_share_of_step": (mlp_ms / world) / (elapsed * 1e3) if world == 1 else None}
+
+
+def pmc_traffic(H, W, kernel="mlp_fused_kernel"):
     """Measured HBM bytes per MLP launch from the newest committed PMC summary
     (tools/pmc.sh + tools/pmc_summary.py) taken on this same workload, else None."""
     import glob
@@ -157,7 +196,7 @@ def pmc_traffic(H, W):
         with open(f) as fh:
             doc = json.load(fh)
         wl = doc.get("workload", {})
-        e = doc.get("kernels", {}).get("mlp_fused", {})
+        e = doc.get("kernels", {}).get(kernel.replace("_kernel", ""), {})
         if wl.get("H") == H and wl.get("W") == W and "hbm_bytes_per_launch" in e:
             best = e["hbm_bytes_per_launch"]
     return best

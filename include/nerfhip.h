@@ -72,6 +72,16 @@ int nerf_mlp_forward(const float* w_slices, const float* w_head,
                      const float* z, int64_t z_stride, int64_t n, int S,
                      float* raw, nerf_stream_t stream);
 
+/* Same contract as nerf_mlp_forward, computed with a 3-term FP16 split of the
+ * FP32 operands on FP16 MFMA (w*x = wh*xh + wh*xl + wl*xh, exact products,
+ * FP32 accumulation; power-of-two scaling keeps the splits in FP16 range):
+ * ~2^-22 relative per product, 5.3x the FP32 MFMA arithmetic rate.
+ * w_slices/w_head: packed by nerfhip.pack.pack_mlp_x3 (device). */
+int nerf_mlp_forward_x3(const float* w_slices, const float* w_head,
+                        const float* rays_o, const float* rays_d,
+                        const float* z, int64_t z_stride, int64_t n, int S,
+                        float* raw, nerf_stream_t stream);
+
 /* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
  * Reductions follow torch's CPU float32 summation order.
  * Outputs rgb[n][3], disp/acc/depth[n]; weights[n][S] optional (NULL). */

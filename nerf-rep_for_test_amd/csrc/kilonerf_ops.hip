@@ -139,40 +139,64 @@ __global__ __launch_bounds__(FF_BLOCK) void kn_fourier_kernel(const float* __res
 // ---------------------------------------------------------------------------
 // integrate + replace_transparency_by_background_color (integrate.cu:9-112)
 // ---------------------------------------------------------------------------
-__global__ void kn_integrate_kernel(const float4* __restrict__ rgb_sigma,
-                                    const float* __restrict__ dists, float* __restrict__ rgb_map,
-                                    float* __restrict__ acc_map, float* __restrict__ trans,
-                                    uint8_t* __restrict__ mask, int num_rays, int spr, float thr,
-                                    int initial) {
-  const int ray = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ray >= num_rays) return;
-  float T = initial ? 1.0f : trans[ray];
-  const bool act = T > thr;
+// One thread per ray, as the reference (its per-sample float recurrence for T
+// is kept bit-for-bit), but each wave stages its 64 rays' samples through LDS
+// in 8-sample chunks: the global loads are whole 128-B lines (8 lanes per ray
+// chunk) instead of 64 rays' scattered 16-B pieces per instruction.
+constexpr int KI_CHUNK = 8;
+constexpr int KI_WAVES = 4;
+
+__global__ __launch_bounds__(64 * KI_WAVES) void kn_integrate_kernel(
+    const float4* __restrict__ rgb_sigma, const float* __restrict__ dists,
+    float* __restrict__ rgb_map, float* __restrict__ acc_map, float* __restrict__ trans,
+    uint8_t* __restrict__ mask, int num_rays, int spr, float thr, int initial) {
+  __shared__ float4 stage[KI_WAVES][64][KI_CHUNK + 1];   // +1: spread the rows over banks
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int ray0 = (blockIdx.x * KI_WAVES + wave) * 64;
+  if (ray0 >= num_rays) return;   // wave-uniform
+  const int ray = ray0 + lane;
+  const bool in = ray < num_rays;
+  float T = in ? (initial ? 1.0f : trans[ray]) : 0.0f;
+  const bool act = in && T > thr;
   float r = 0.f, g = 0.f, b = 0.f, acc = 0.f;
+  if (act && !initial) {
+    r = rgb_map[ray * 3];
+    g = rgb_map[ray * 3 + 1];
+    b = rgb_map[ray * 3 + 2];
+    acc = acc_map[ray];
+  }
+  const float dist = in ? dists[ray] : 0.f;
+  const uint64_t need = __ballot(act);
+  for (int c0 = 0; c0 < spr && need; c0 += KI_CHUNK) {
+    const int cn = spr - c0 < KI_CHUNK ? spr - c0 : KI_CHUNK;
+    // cooperative load: element e = (ray_local, s) with s fastest
+    for (int e = lane; e < 64 * KI_CHUNK; e += 64) {
+      const int rl = e / KI_CHUNK, sl = e % KI_CHUNK;
+      if (sl < cn && ray0 + rl < num_rays && ((need >> rl) & 1))
+        stage[wave][rl][sl] = rgb_sigma[(int64_t)(ray0 + rl) * spr + c0 + sl];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (act) {
+      for (int sl = 0; sl < cn; ++sl) {
+        const float4 v = stage[wave][lane][sl];
+        const float alpha = 1.0f - expf(-v.w * dist);
+        const float w = alpha * T;
+        // `T *= 1.0f - alpha + 1e-10` is evaluated in double (1e-10 is a double literal)
+        T = (float)((double)T * ((double)(1.0f - alpha) + 1e-10));
+        r = __builtin_fmaf(v.x, w, r);
+        g = __builtin_fmaf(v.y, w, g);
+        b = __builtin_fmaf(v.z, w, b);
+        acc = acc + w;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   if (act) {
-    if (!initial) {
-      r = rgb_map[ray * 3];
-      g = rgb_map[ray * 3 + 1];
-      b = rgb_map[ray * 3 + 2];
-      acc = acc_map[ray];
-    }
-    const float dist = dists[ray];
-    const float4* p = rgb_sigma + (int64_t)ray * spr;
-    for (int s = 0; s < spr; ++s) {
-      const float4 v = p[s];
-      const float alpha = 1.0f - expf(-v.w * dist);
-      const float w = alpha * T;
-      // `T *= 1.0f - alpha + 1e-10` is evaluated in double (1e-10 is a double literal)
-      T = (float)((double)T * ((double)(1.0f - alpha) + 1e-10));
-      r = __builtin_fmaf(v.x, w, r);
-      g = __builtin_fmaf(v.y, w, g);
-      b = __builtin_fmaf(v.z, w, b);
-      acc = acc + w;
-    }
     trans[ray] = T;
     if (T <= thr) mask[ray] = 0;
   }
-  if (act || initial) {
+  if (act || (in && initial)) {
     rgb_map[ray * 3] = r;
     rgb_map[ray * 3 + 1] = g;
     rgb_map[ray * 3 + 2] = b;
@@ -563,7 +587,8 @@ int kn_integrate(const float* rgb_sigma, const float* dists, float* rgb_map, flo
                "kn_integrate: null pointer");
   NERF_REQUIRE(num_rays >= 0 && spr >= 0, "kn_integrate: bad size");
   if (num_rays == 0) return 0;
-  hipLaunchKernelGGL(kn_integrate_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(kn_integrate_kernel, dim3((unsigned)cdiv(num_rays, 64 * KI_WAVES)),
+                     dim3(64 * KI_WAVES), 0,
                      as_stream(stream), (const float4*)rgb_sigma, dists, rgb_map, acc_map,
                      transmittance, mask, num_rays, spr, thr, initial);
   return check_launch("kn_integrate_kernel");

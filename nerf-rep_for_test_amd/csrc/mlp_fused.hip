@@ -19,103 +19,55 @@
 //   Per wave: 64 activation VGPRs + 64 accumulator AGPRs, so two waves fit per
 //   SIMD and fragment reads are prefetched one MFMA group ahead.
 //
-// Weight streaming
+// Weight streaming (mlp_stream.h)
 //   The packed network is 73 slices of 32 KiB (32 "blocks" of 64 lanes x 16 B:
 //   one ds_read_b128 per lane = 4 consecutive k-steps of one 16-row tile).
-//   Slices stream L2 -> LDS with global_load_lds_dwordx4 into a 2-deep ring
-//   (two LDS arrays, statically selected), one barrier per slice; 128 MFMAs per
-//   wave (2 x 4096 cycles per SIMD) per slice hide the next slice's load.
+//   Slices stream L2 -> LDS with global_load_lds_dwordx4 into a 4-deep ring,
+//   issued three slices ahead; one counted vmcnt + s_barrier per slice.
 //   Density (1x256) and rgb (3x128) heads run on the VALU (fma chains + a
 //   4-lane butterfly) instead of padding 15/13 of 16 MFMA rows.
 #include "common.h"
+#include "mlp_stream.h"
 
 namespace nerfhip {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kWaves = 8;
+constexpr int kWaves = kStreamWaves;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kTile = 16 * kWaves;            // samples per workgroup
-constexpr int kSliceFloats = NERF_MLP_SLICE_FLOATS;
-constexpr int kSlices = NERF_MLP_SLICES;
-constexpr int kHeadFloats = NERF_MLP_HEAD_FLOATS;
-constexpr int kBlocksPerWave = 32 / kWaves;   // glds pieces each wave stages per slice
-
-// head block layout (floats); bias/weight vectors are lane-group packed:
-// element [g4][4m + r] belongs to output feature 16m + 4*g4 + r.
-constexpr int kHeadBias = 0;          // layers 0..8 (pts 0..7, feature): [9][4][64]
-constexpr int kHeadBiasViews = 2304;  // [4][32]
-constexpr int kHeadAlphaW = 2432;     // [4][64]
-constexpr int kHeadAlphaB = 2688;     // [1]
-constexpr int kHeadRgbW = 2692;       // [3][4][32]
-constexpr int kHeadRgbB = 3076;       // [3]
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-// Ablation switches for timing-only builds (tools/mlp_ablate.py); the shipped
-// library defines none of them. ABL_NOBAR drops the per-slice barriers,
-// ABL_NODMA the weight staging, ABL_NOENC the sin/cos, ABL_NOEPI the bias/ReLU.
-// One 1-KiB LDS-DMA piece (of the 4 each wave stages per slice): block
-// wave*4 + j of slice `src` into the same block of LDS buffer `dst`.
-__device__ __forceinline__ void stage_piece(const float4* src, float* dst, int wave, int lane,
-                                            int j) {
-#if defined(ABL_NODMA)
-  return;
-#endif
-  const int b = wave * kBlocksPerWave + j;
-  __builtin_amdgcn_global_load_lds((const void*)(src + b * 64 + lane),
-                                   (lds_ptr_t)(dst + b * 256), 16, 0, 0);
-}
-
-// DMA of one future slice, spread over the MFMA groups of the current one.
-struct Dma {
-  const float4* src;   // slice in HBM/L2, or nullptr when there is none to stage
-  float* dst;          // its LDS ring buffer
-  int wave, lane;
-};
-
-__device__ __forceinline__ float4 frag(const float* buf, int block, int lane) {
-  return *reinterpret_cast<const float4*>(buf + (block * 64 + lane) * 4);
-}
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
-#define SCHED_DS_READ 0x100
-#define SCHED_MFMA 0x008
 
-// One group = 8 MFMAs: two 16-row tiles x the 4 k-steps of one quad.
+// One group = 8 MFMAs: two 16-row tiles x the 4 k-steps of one quad; `mid`
+// runs between the 4th and 5th MFMA (pinned there by sched barriers).
+template <typename Mid>
 __device__ __forceinline__ void mfma_group(f32x4& c0, f32x4& c1, const float4& a0,
-                                           const float4& a1, const f32x4& bv) {
+                                           const float4& a1, const f32x4& bv, Mid mid) {
   c0 = MFMA(a0.x, bv[0], c0);
   c1 = MFMA(a1.x, bv[0], c1);
   c0 = MFMA(a0.y, bv[1], c0);
   c1 = MFMA(a1.y, bv[1], c1);
+  __builtin_amdgcn_sched_barrier(0);
+  mid();
+  __builtin_amdgcn_sched_barrier(0);
   c0 = MFMA(a0.z, bv[2], c0);
   c1 = MFMA(a1.z, bv[2], c1);
   c0 = MFMA(a0.w, bv[3], c0);
   c1 = MFMA(a1.w, bv[3], c1);
 }
 
-// LDS fragment reads are issued as inline asm: hipcc neither tracks nor waits
-// for them, so the schedule below owns every lgkmcnt wait of the slice loop
-// (hipcc's own waits there are lgkmcnt(0) placed after the next group's reads,
-// which serialises the LDS latency with the MFMAs). One per-lane base address
-// per buffer; the block offset is an instruction immediate.
-__device__ __forceinline__ unsigned lds_base(const float* buf, int lane) {
-  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(buf) +
-         (unsigned)(lane * 16);
-}
-
-template <int BLOCK>
-__device__ __forceinline__ float4 frag_async(unsigned base) {
-  f32x4 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(BLOCK * 1024) : "memory");
-  return make_float4(v[0], v[1], v[2], v[3]);
-}
-
-__device__ __forceinline__ void lds_drain() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);   // keep MFMAs behind the wait (guide rule 18)
-}
+// Where each wave issues its 4 weight-DMA pieces per slice (timing knobs, see
+// tools/mlp_ablate.py): MLP_DMA_POS 0 = after the group's LDS drain, 1 = after
+// its fragment reads, 2 = between its MFMAs, 3 = after its MFMAs;
+// MLP_DMA_EVERY = group spacing of the pieces (from group MLP_DMA_FIRST).
+#ifndef MLP_DMA_POS
+#define MLP_DMA_POS 0
+#endif
+#ifndef MLP_DMA_EVERY
+#define MLP_DMA_EVERY 2
+#endif
+#ifndef MLP_DMA_FIRST
+#define MLP_DMA_FIRST 0
+#endif
 
 // Group G of NG over blocks 2G, 2G+1: drain group G's reads (issued one group
 // earlier), issue group G+1's into the other named register pair, then group
@@ -124,10 +76,16 @@ template <int G, int NG, typename Cfg, typename Acc, typename BV>
 __device__ __forceinline__ void run_group(Acc& acc, unsigned base, const BV& bv, float4& x0,
                                           float4& x1, float4& y0, float4& y1, const Dma& dma) {
   if constexpr (G < NG) {
+    constexpr bool kDma = G >= MLP_DMA_FIRST && (G - MLP_DMA_FIRST) % MLP_DMA_EVERY == 0 &&
+                          (G - MLP_DMA_FIRST) / MLP_DMA_EVERY < kBlocksPerWave;
+    constexpr int kPiece = (G - MLP_DMA_FIRST) / MLP_DMA_EVERY;
+    auto piece = [&]() {
+      if constexpr (kDma) {
+        if (dma.src) stage_piece(dma.src, dma.dst, dma.wave, dma.lane, kPiece);
+      }
+    };
     lds_drain();
-    if constexpr ((G & 1) == 0 && G < 2 * kBlocksPerWave) {
-      if (dma.src) stage_piece(dma.src, dma.dst, dma.wave, dma.lane, G / 2);
-    }
+    if constexpr (MLP_DMA_POS == 0) piece();
     if constexpr (G + 1 < NG) {
       if constexpr ((G & 1) == 0) {
         y0 = frag_async<2 * G + 2>(base);
@@ -137,12 +95,18 @@ __device__ __forceinline__ void run_group(Acc& acc, unsigned base, const BV& bv,
         x1 = frag_async<2 * G + 3>(base);
       }
     }
+    if constexpr (MLP_DMA_POS == 1) piece();
     __builtin_amdgcn_sched_barrier(0);
     constexpr int m = Cfg::tile(G);
+    auto mid = [&]() {
+      if constexpr (MLP_DMA_POS == 2) piece();
+    };
     if constexpr ((G & 1) == 0)
-      mfma_group(acc[m], acc[m + 1], x0, x1, bv[Cfg::bsel(G)]);
+      mfma_group(acc[m], acc[m + 1], x0, x1, bv[Cfg::bsel(G)], mid);
     else
-      mfma_group(acc[m], acc[m + 1], y0, y1, bv[Cfg::bsel(G)]);
+      mfma_group(acc[m], acc[m + 1], y0, y1, bv[Cfg::bsel(G)], mid);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MLP_DMA_POS == 3) piece();
     __builtin_amdgcn_sched_barrier(0);
     run_group<G + 1, NG, Cfg>(acc, base, bv, x0, x1, y0, y1, dma);
   }
@@ -183,37 +147,6 @@ template <int NQ, int Q0, typename BV>
 __device__ __forceinline__ void slice128(f32x4 (&acc)[8], const float* buf, const BV& b,
                                          int lane, const Dma& dma) {
   run_groups<4 * NQ, Slice128<Q0>>(acc, buf, lane, b, dma);
-}
-
-// 4-deep slice ring: while slice g is computed, slices g+1 and g+2 are landed
-// or landing and slice g+3 is being staged into buffer (g+3)%4 (freed by the
-// barrier that ended slice g-1). At the end of slice g each wave waits only for
-// its own DMA of slice g+1 (counted vmcnt: the pieces of g+2 and g+3 may stay
-// in flight), then one raw s_barrier makes slice g+1 visible to all waves.
-struct Ring {
-  float* base;                     // 4 x kSliceFloats
-  const float4* slices;            // packed network in HBM
-  int wave, lane;
-  __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
-  __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
-    const int t = g + 3;
-    return Dma{t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t), wave,
-               lane};
-  }
-};
-
-template <int PENDING>   // slices (of 4 pieces) allowed to stay in flight
-__device__ __forceinline__ void slice_end() {
-#if !defined(ABL_NOBAR)
-  if constexpr (PENDING >= 2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (PENDING == 1)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#endif
-  __builtin_amdgcn_sched_barrier(0);
 }
 
 // Frequency encoding in the kernel's K order (see header) for lane group g4.
@@ -273,13 +206,6 @@ __device__ __forceinline__ void layer_body(f32x4 (&acc)[16], const f32x4 (&act)[
   slice256<5>(acc, R.buf(g + 5), act, R.lane, R.dma_for(g + 5)); slice_end<2>();
   slice256<6>(acc, R.buf(g + 6), act, R.lane, R.dma_for(g + 6)); slice_end<2>();
   slice256<7>(acc, R.buf(g + 7), act, R.lane, R.dma_for(g + 7)); slice_end<2>();
-}
-
-// sum over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48);
-// every lane of the quad ends with the bitwise-same value
-__device__ __forceinline__ float quad_sum(float v) {
-  v = v + __shfl_xor(v, 16);
-  return v + __shfl_xor(v, 32);
 }
 
 __global__ __launch_bounds__(kThreads, 2) void mlp_fused_kernel(

@@ -1,0 +1,113 @@
+// Weight streaming shared by the fused MLP kernels (mlp_fused.hip: FP32 MFMA,
+// mlp_x3.hip: 3-term FP16 split MFMA): a packed network of 73 slices of
+// 32 KiB (32 blocks of 64 lanes x 16 B) streams L2 -> LDS by LDS-DMA through a
+// 4-deep ring while 8 waves multiply the resident slice; fragments are read
+// with inline-asm ds_read_b128 at immediate block offsets.
+#pragma once
+
+#include "common.h"
+
+namespace nerfhip {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kSliceFloats = NERF_MLP_SLICE_FLOATS;
+constexpr int kSlices = NERF_MLP_SLICES;
+constexpr int kHeadFloats = NERF_MLP_HEAD_FLOATS;
+constexpr int kStreamWaves = 8;                     // waves per workgroup
+constexpr int kBlocksPerWave = 32 / kStreamWaves;   // glds pieces each wave stages per slice
+
+// head block layout (floats); bias/weight vectors are lane-group packed:
+// element [g4][4m + r] belongs to output feature 16m + 4*g4 + r.
+constexpr int kHeadBias = 0;          // layers 0..8 (pts 0..7, feature): [9][4][64]
+constexpr int kHeadBiasViews = 2304;  // [4][32]
+constexpr int kHeadAlphaW = 2432;     // [4][64]
+constexpr int kHeadAlphaB = 2688;     // [1]
+constexpr int kHeadRgbW = 2692;       // [3][4][32]
+constexpr int kHeadRgbB = 3076;       // [3]
+constexpr int kHeadScales = 3080;     // mlp_x3: per-layer weight scale exponents [10]
+
+// Ablation switches for timing-only builds (tools/mlp_ablate.py); the shipped
+// library defines none of them. ABL_NOBAR drops the per-slice barriers,
+// ABL_NODMA the weight staging, ABL_NOENC the sin/cos, ABL_NOEPI the bias/ReLU.
+// One 1-KiB LDS-DMA piece (of the 4 each wave stages per slice): block
+// wave*4 + j of slice `src` into the same block of LDS buffer `dst`.
+__device__ __forceinline__ void stage_piece(const float4* src, float* dst, int wave, int lane,
+                                            int j) {
+#if defined(ABL_NODMA)
+  return;
+#endif
+  const int b = wave * kBlocksPerWave + j;
+  __builtin_amdgcn_global_load_lds((const void*)(src + b * 64 + lane),
+                                   (lds_ptr_t)(dst + b * 256), 16, 0, 0);
+}
+
+// DMA of one future slice, spread over the MFMA groups of the current one.
+struct Dma {
+  const float4* src;   // slice in HBM/L2, or nullptr when there is none to stage
+  float* dst;          // its LDS ring buffer
+  int wave, lane;
+};
+
+// LDS fragment reads are issued as inline asm: hipcc neither tracks nor waits
+// for them, so the schedule below owns every lgkmcnt wait of the slice loop
+// (hipcc's own waits there are lgkmcnt(0) placed after the next group's reads,
+// which serialises the LDS latency with the MFMAs). One per-lane base address
+// per buffer; the block offset is an instruction immediate.
+__device__ __forceinline__ unsigned lds_base(const float* buf, int lane) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(buf) +
+         (unsigned)(lane * 16);
+}
+
+template <int BLOCK>
+__device__ __forceinline__ float4 frag_async(unsigned base) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "i"(BLOCK * 1024) : "memory");
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void lds_drain() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);   // keep MFMAs behind the wait (guide rule 18)
+}
+
+// 4-deep slice ring: while slice g is computed, slices g+1 and g+2 are landed
+// or landing and slice g+3 is being staged into buffer (g+3)%4 (freed by the
+// barrier that ended slice g-1). At the end of slice g each wave waits only for
+// its own DMA of slice g+1 (counted vmcnt: the pieces of g+2 and g+3 may stay
+// in flight), then one raw s_barrier makes slice g+1 visible to all waves.
+struct Ring {
+  float* base;                     // 4 x kSliceFloats
+  const float4* slices;            // packed network in HBM
+  int wave, lane;
+  __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
+  __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
+    const int t = g + 3;
+    return Dma{t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t), wave,
+               lane};
+  }
+};
+
+template <int PENDING>   // slices (of 4 pieces) allowed to stay in flight
+__device__ __forceinline__ void slice_end() {
+#if !defined(ABL_NOBAR)
+  if constexpr (PENDING >= 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (PENDING == 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#endif
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// sum over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48);
+// every lane of the quad ends with the bitwise-same value
+__device__ __forceinline__ float quad_sum(float v) {
+  v = v + __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+}  // namespace nerfhip

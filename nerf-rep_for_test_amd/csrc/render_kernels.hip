@@ -339,18 +339,23 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
     L.zf[j] = v;
   }
   __builtin_amdgcn_wave_barrier();
-  // ascending bitonic sort of the (inf-padded) fine samples
-  for (int k = 2; k <= p2; k <<= 1) {
-    for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int i = lane; i < p2; i += 64) {
-        const int prt = i ^ jj;
-        if (prt > i) {
-          const float x = L.zf[i], y = L.zf[prt];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) { L.zf[i] = y; L.zf[prt] = x; }
+  // ascending bitonic sort of the (inf-padded) fine samples, skipped when the
+  // inverse CDF of sorted u (eval: linspace) already produced them in order
+  bool unsorted = false;
+  for (int j = lane; j + 1 < n_imp; j += 64) unsorted |= L.zf[j] > L.zf[j + 1];
+  if (__ballot(unsorted)) {
+    for (int k = 2; k <= p2; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        for (int i = lane; i < p2; i += 64) {
+          const int prt = i ^ jj;
+          if (prt > i) {
+            const float x = L.zf[i], y = L.zf[prt];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) { L.zf[i] = y; L.zf[prt] = x; }
+          }
         }
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
     }
   }
   // torch.sort(cat(z, z_fine)) values: merge by rank (ties: coarse first; equal

@@ -229,3 +229,208 @@ def emulate(slices, head, pts, dirs):
     rgb = np.stack([np.einsum("f,fp->p", _group_pack_inv(hd[H_RGB_W + c * 128:H_RGB_W + c * 128 + 128], 8), v)
                     + hd[H_RGB_B + c] for c in range(3)], -1)
     return np.concatenate([rgb, alpha[:, None]], -1)
+
+
+# ----------------------------------------------------------------------------
+# 3-term FP16 split layout (csrc/mlp_x3.hip, v_mfma_f32_16x16x32_f16)
+# ----------------------------------------------------------------------------
+H_SCALES = 3080          # per-layer weight scale exponents [10] (layers 0..8, views)
+X3_GROUPS, X3_J = 4, 8   # lane groups x slots per lane of one 32-deep K step
+
+
+def x3_cols_act(nq=8):
+    """[nq, 4, 8]: K step q, lane group g, slot j -> previous-layer feature
+    16*(2q + j//4) + 4g + j%4 (registers j%4 of accumulator tiles 2q, 2q+1)."""
+    q, g, j = np.meshgrid(np.arange(nq), np.arange(4), np.arange(8), indexing="ij")
+    return 16 * (2 * q + (j >> 2)) + 4 * g + (j & 3)
+
+
+def x3_cols_enc():
+    """[2, 4, 8] for the xyz encoding (63 features, freq.py column order):
+    slot i = 8q + j of group g = sin (i even) / cos (i odd) of pair 8g + i//2 =
+    (band f, coord c) = divmod(pair, 3); group 3 slots 12..14 = x, y, z."""
+    out = np.full((2, 4, 8), -1)
+    for g in range(4):
+        for i in range(16):
+            q, j = divmod(i, 8)
+            pr = 8 * g + (i >> 1)
+            if pr < 30:
+                f, c = divmod(pr, 3)
+                out[q, g, j] = 3 + 6 * f + c + (3 if i & 1 else 0)
+            elif g == 3 and 12 <= i <= 14:
+                out[q, g, j] = i - 12
+    return out
+
+
+def x3_cols_dir():
+    """[1, 4, 8] for the view encoding (27 features): slots 2t, 2t+1 of group g
+    = sin, cos of (band g, coord t); slot 6 = raw coord g (g < 3)."""
+    out = np.full((1, 4, 8), -1)
+    for g in range(4):
+        for t in range(3):
+            out[0, g, 2 * t] = 3 + 6 * g + t
+            out[0, g, 2 * t + 1] = 6 + 6 * g + t
+        if g < 3:
+            out[0, g, 6] = g
+    return out
+
+
+def _x3_layer_cols(kind):
+    act = x3_cols_act()
+    if kind == "l0":
+        return x3_cols_enc()
+    if kind == "act":
+        return act
+    if kind == "skip":
+        return np.concatenate([x3_cols_enc(), IN_XYZ + act], 0)
+    if kind == "views":
+        d = x3_cols_dir()
+        return np.concatenate([act, np.where(d >= 0, W + d, -1)], 0)
+    raise ValueError(kind)
+
+
+def weight_exponent(Wt):
+    """sw with max|W| * 2^sw in [2^11, 2^12) (0 for an all-zero matrix)."""
+    m = float(np.abs(Wt).max())
+    if m == 0.0:
+        return 0
+    return 12 - int(np.frexp(m)[1])
+
+
+def f16_split(x):
+    h = x.astype(np.float16)
+    lo = (x - h.astype(np.float32)).astype(np.float16)
+    return h, lo
+
+
+def _x3_frags(Ws, cols, tiles):
+    """[steps, tiles, 2 (hi, lo), 64, 8] float16 A fragments of scaled W [out, in]."""
+    Wp = np.concatenate([Ws, np.zeros((Ws.shape[0], 1), np.float32)], 1)
+    lane = np.arange(64)
+    c = cols[:, lane >> 4, :]                                       # [Q, 64, 8]
+    c = np.where(c < 0, Ws.shape[1], c)
+    rows = TILE * np.arange(tiles)[:, None] + (lane & 15)[None, :]  # [T, 64]
+    vals = Wp[rows[None, :, :, None], c[:, None, :, :]]             # [Q, T, 64, 8]
+    h, lo = f16_split(vals.astype(np.float32))
+    return np.stack([h, lo], 2)
+
+
+def pack_mlp_x3(params, prefix="model"):
+    """Packed network for nerf_mlp_forward_x3: (slices float32[73*8192] holding
+    FP16 fragment pairs, head float32[3200])."""
+    def get(name):
+        v = params[f"{prefix}.{name}"]
+        v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
+        return np.ascontiguousarray(v, np.float32)
+
+    _, head = pack_mlp(params, prefix)          # biases and VALU heads: same layout
+    slices = []
+    for li, (name, kind, tiles) in enumerate(layer_plan()):
+        Wt = get(name + ".weight")
+        sw = weight_exponent(Wt)
+        head[H_SCALES + li] = sw
+        cols = _x3_layer_cols(kind)
+        assert cols.max() < Wt.shape[1], (name, cols.max(), Wt.shape)
+        fr = _x3_frags((Wt * np.float32(2.0 ** sw)).astype(np.float32), cols, tiles)
+        if tiles == 16:                          # one K step per slice: block 2m + part
+            for q in range(fr.shape[0]):
+                slices.append(fr[q].reshape(32, 64, 8))
+        else:                                    # views: two steps per slice, then dir
+            for q0 in range(0, fr.shape[0], 2):
+                blk = np.zeros((32, 64, 8), np.float16)
+                for qq in range(min(2, fr.shape[0] - q0)):
+                    blk[16 * qq:16 * qq + 16] = fr[q0 + qq].reshape(16, 64, 8)
+                slices.append(blk)
+    assert len(slices) == SLICES, len(slices)
+    allh = np.stack(slices).reshape(-1)
+    return np.ascontiguousarray(allh).view(np.float32).copy(), head
+
+
+def _x3_decode(slices):
+    return slices.view(np.float16).reshape(SLICES, 32, 64, 8).astype(np.float64)
+
+
+def emulate_x3(slices, head, pts, dirs):
+    """numpy dataflow of mlp_x3_kernel with exact products (CPU tests of the layout
+    and the per-sample power-of-two scaling). pts, dirs: [P, 3]."""
+    blk = _x3_decode(slices)
+    hd = head.astype(np.float64)
+    P = pts.shape[0]
+    enc_feat = O_embed(pts, 10)                   # [P, 63] reference column order
+    dir_feat = O_embed(dirs, 4)                   # [P, 27]
+    ce, cd, ca = x3_cols_enc(), x3_cols_dir(), x3_cols_act()
+
+    def gather(feat, cols):                       # -> [Q, 32 (k = 8g + j), P]
+        f = np.concatenate([feat, np.zeros((P, 1))], 1)
+        c = np.where(cols < 0, feat.shape[1], cols).reshape(cols.shape[0], 32)
+        return f[:, c].transpose(1, 2, 0)
+
+    def split(x, s):                              # x [Q, 32, P], s [P]
+        xs = (x * s[None, None, :]).astype(np.float32)
+        h, lo = f16_split(xs)
+        return h.astype(np.float64), lo.astype(np.float64)
+
+    def mm(slice_ids, blocks_of, B_h, B_l, tiles):
+        acc = np.zeros((tiles * 16, P))
+        for si, (sl, q_local) in enumerate(zip(slice_ids, blocks_of)):
+            for m in range(tiles):
+                b = q_local + 2 * m
+                Ah = blk[sl, b].reshape(4, 16, 8).transpose(1, 0, 2).reshape(16, 32)
+                Al = blk[sl, b + 1].reshape(4, 16, 8).transpose(1, 0, 2).reshape(16, 32)
+                acc[16 * m:16 * m + 16] += Ah @ B_h[si] + Ah @ B_l[si] + Al @ B_h[si]
+        return acc
+
+    def exponent(mx):                             # per sample: mx [P]
+        return np.where(mx > 0, 14 - np.frexp(mx)[1], 0).astype(np.float64)
+
+    def bias_of(off, tiles):
+        return _group_pack_inv(hd[off:off + 64 * tiles // 4 * 1], tiles)
+
+    g = 0
+    e = exponent(np.abs(enc_feat).max(1))
+    Eh, El = split(gather(enc_feat, ce), 2.0 ** e)
+    acc = mm([0, 1], [0, 0], Eh, El, 16)
+    h = np.maximum(acc * 2.0 ** -(hd[H_SCALES] + e) + bias_of(H_BIAS, 16)[:, None], 0)
+    g = 2
+    alpha = None
+    for L in range(1, 9):
+        x = h.T                                   # [P, 256] features
+        mx = np.abs(x).max(1)
+        if L == 5:
+            mx = np.maximum(mx, np.abs(enc_feat).max(1))
+        e = exponent(mx)
+        Xh, Xl = split(gather(x, ca), 2.0 ** e)
+        acc = np.zeros((256, P))
+        if L == 5:
+            Eh, El = split(gather(enc_feat, ce), 2.0 ** e)
+            acc += mm([g, g + 1], [0, 0], Eh, El, 16)
+            g += 2
+        acc += mm(list(range(g, g + 8)), [0] * 8, Xh, Xl, 16)
+        g += 8
+        h = acc * 2.0 ** -(hd[H_SCALES + L] + e) + bias_of(H_BIAS + L * 256, 16)[:, None]
+        if L != 8:
+            h = np.maximum(h, 0)
+        if L == 7:
+            aw = _group_pack_inv(hd[H_ALPHA_W:H_ALPHA_W + 256], 16)
+            alpha = aw @ h + hd[H_ALPHA_B]
+    x = h.T
+    e = exponent(np.maximum(np.abs(x).max(1), np.abs(dir_feat).max(1)))
+    Xh, Xl = split(gather(x, ca), 2.0 ** e)
+    Dh, Dl = split(gather(dir_feat, cd), 2.0 ** e)
+    ids = [g + k // 2 for k in range(8)]
+    offs = [16 * (k % 2) for k in range(8)]
+    acc = mm(ids, offs, Xh, Xl, 8) + mm([g + 4], [0], Dh, Dl, 8)
+    v = np.maximum(acc * 2.0 ** -(hd[H_SCALES + 9] + e)
+                   + _group_pack_inv(hd[H_BIAS_VIEWS:H_BIAS_VIEWS + 128], 8)[:, None], 0)
+    rgb = np.stack([_group_pack_inv(hd[H_RGB_W + c * 128:H_RGB_W + c * 128 + 128], 8) @ v
+                    + hd[H_RGB_B + c] for c in range(3)], -1)
+    return np.concatenate([rgb, alpha[:, None]], -1)
+
+
+def O_embed(x, n_freq):
+    """freq.py:7-32 column order [x, sin(2^0 x), cos(2^0 x), ...] in float64."""
+    x = np.asarray(x, np.float64)
+    out = [x]
+    for f in range(n_freq):
+        out += [np.sin(x * 2.0 ** f), np.cos(x * 2.0 ** f)]
+    return np.concatenate(out, -1)

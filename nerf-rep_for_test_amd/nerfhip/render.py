@@ -18,7 +18,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
-from .pack import pack_mlp
+from .pack import pack_mlp, pack_mlp_x3
 
 REF_CHUNK = 2048            # VR:147 ray chunk (ERT/ESS semantics)
 GRID_BBOX = (-2.0, 2.0)     # VR:842-843
@@ -32,13 +32,17 @@ def coarse_depth_table(near, far, n_samples, lindisp):
     return 1. / (1. / near * (1. - t_vals) + 1. / far * t_vals)
 
 
+MLP_KERNELS = {"fp32": ("nerf_mlp_forward", pack_mlp),
+               "f16x3": ("nerf_mlp_forward_x3", pack_mlp_x3)}
+
+
 class NerfPipeline:
     """Packed weights + constant tables resident on one GPU; renders rays/frames."""
 
     def __init__(self, device, N_samples=64, N_importance=128, near=2.0, far=6.0,
                  lindisp=False, white_bkgd=True, enable_ess=False, enable_ert=False,
                  ert_threshold=0.05, ess_skip_threshold=0.5, grid_update_interval=500,
-                 max_rays_per_pass=1 << 20):
+                 max_rays_per_pass=1 << 20, mlp_precision="f16x3"):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise _lib.NerfHipError("NerfPipeline needs a ROCm GPU device (no CPU fallback)")
@@ -53,6 +57,11 @@ class NerfPipeline:
         self.grid_update_interval = int(grid_update_interval)
         self.grid_update_counter = 0
         self.max_rays_per_pass = int(max_rays_per_pass)
+        # "fp32": FP32 MFMA (mlp_fused.hip); "f16x3": 3-term FP16 split of the FP32
+        # operands on FP16 MFMA (mlp_x3.hip), ~2^-22 relative per product
+        if mlp_precision not in MLP_KERNELS:
+            raise ValueError(f"mlp_precision must be one of {sorted(MLP_KERNELS)}")
+        self.mlp_precision = mlp_precision
         self.z_base = coarse_depth_table(self.near, self.far, self.N_samples,
                                          self.lindisp).to(self.device)
         self.u_eval = (torch.linspace(0., 1., steps=self.N_importance).to(self.device)
@@ -67,7 +76,7 @@ class NerfPipeline:
     def set_weights(self, params, coarse_prefix="model", fine_prefix="model_fine"):
         """params: name -> tensor/array (reference state_dict names)."""
         def up(prefix):
-            sl, hd = pack_mlp(params, prefix)
+            sl, hd = MLP_KERNELS[self.mlp_precision][1](params, prefix)
             return (torch.from_numpy(sl).to(self.device), torch.from_numpy(hd).to(self.device))
         self.coarse = up(coarse_prefix)
         self.fine = up(fine_prefix) if self.N_importance > 0 else None
@@ -96,7 +105,7 @@ class NerfPipeline:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        call("nerf_mlp_forward", ptr(packed[0]), ptr(packed[1]), ptr(rays_o), ptr(rays_d),
+        call(MLP_KERNELS[self.mlp_precision][0], ptr(packed[0]), ptr(packed[1]), ptr(rays_o), ptr(rays_d),
              ptr(z), z_stride, n, S, ptr(raw), _lib.stream_of(self.device))
         if t is not None:
             e1.record()

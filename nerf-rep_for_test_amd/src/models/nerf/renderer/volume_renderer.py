@@ -56,7 +56,10 @@ class Renderer:
             self.device, N_samples=self.N_samples, N_importance=self.N_importance,
             near=self.near, far=self.far, lindisp=self.lindisp, white_bkgd=self.white_bkgd,
             enable_ess=self.enable_ess, enable_ert=self.enable_ert,
-            ert_threshold=self.ert_threshold)
+            ert_threshold=self.ert_threshold,
+            # not a reference key: "f16x3" (default, FP32 operands as 3-term FP16
+            # splits on FP16 MFMA) or "fp32" (FP32 MFMA); both meet the same parity
+            mlp_precision=getattr(cfg, "mlp_precision", "f16x3"))
         self._weights_key = None
         self.scene_bbox_min = torch.tensor([-2.0, -2.0, -2.0], device=self.device)
         self.scene_bbox_max = torch.tensor([2.0, 2.0, 2.0], device=self.device)

@@ -64,7 +64,8 @@ def test_rays_row_band(dev):
 
 @pytest.mark.parametrize("n,S,stride0", [(1, 64, True), (3, 64, False), (37, 192, False),
                                          (130, 64, True), (2, 7, False)])
-def test_mlp_matches_oracle(dev, n, S, stride0):
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_mlp_matches_oracle(dev, n, S, stride0, prec):
     z = load("f1_c2_crop")
     p = params_of(z)
     rng = np.random.default_rng(n * 1000 + S)
@@ -77,7 +78,7 @@ def test_mlp_matches_oracle(dev, n, S, stride0):
         zr = np.broadcast_to(zz, (n, S))
     else:
         zr = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
-    pipe = _pipe(dev, N_samples=S, N_importance=0)
+    pipe = _pipe(dev, N_samples=S, N_importance=0, mlp_precision=prec)
     pipe.set_weights(p)
     raw = pipe.mlp(pipe.coarse, _t(ro, dev), _t(rd, dev), _t(zz if stride0 else zr, dev),
                    0 if stride0 else S, n, S).cpu().numpy().reshape(n, S, 4)
@@ -87,19 +88,40 @@ def test_mlp_matches_oracle(dev, n, S, stride0):
     assert (np.abs(raw - ref).reshape(-1, 4) / scale).max() < 1e-5
 
 
-def test_mlp_dense_weights(dev):
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_mlp_dense_weights(dev, prec):
     """gain-3 weights (large activations): same channel-relative bound."""
     z = load("f2b_c2_dense")
     p = params_of(z)
     oro, ord_ = O.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     n = 200
     zc = np.broadcast_to(O.coarse_depths(2.0, 6.0, 64, False), (n, 64))
-    pipe = _pipe(dev, N_samples=64, N_importance=0)
+    pipe = _pipe(dev, N_samples=64, N_importance=0, mlp_precision=prec)
     pipe.set_weights(p)
     raw = pipe.mlp(pipe.coarse, _t(oro[:n], dev), _t(ord_[:n], dev), pipe.z_base, 0, n, 64)
     pts = (oro[:n, None, :] + ord_[:n, None, :] * zc[:, :, None]).astype(np.float32)
     ref = O.query_network(pts, ord_[:n], p, "model").reshape(-1, 4)
     scale = np.maximum(1.0, np.abs(ref).max(0))
+    assert (np.abs(raw.cpu().numpy() - ref) / scale).max() < 1e-5
+
+
+@pytest.mark.parametrize("gain", [0.05, 8.0])
+def test_mlp_x3_extreme_weight_scales(dev, gain):
+    """3-term FP16 split at tiny and at large activations (power-of-two scaling)."""
+    from nerfhip.synthetic import make_params
+    p = make_params(5, gain, 0.5)
+    rng = np.random.default_rng(5)
+    n, S = 64, 64
+    ro = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    rd = rng.normal(size=(n, 3)).astype(np.float32)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    zr = np.sort(rng.uniform(0.5, 3, (n, S)), 1).astype(np.float32)
+    pipe = _pipe(dev, N_samples=S, N_importance=0, mlp_precision="f16x3")
+    pipe.set_weights(p)
+    raw = pipe.mlp(pipe.coarse, _t(ro, dev), _t(rd, dev), _t(zr, dev), S, n, S)
+    pts = (ro[:, None, :] + rd[:, None, :] * zr[:, :, None]).astype(np.float32)
+    ref = O.query_network(pts, rd, p, "model").reshape(-1, 4)
+    scale = np.maximum(np.abs(ref).max(0), 1e-30)
     assert (np.abs(raw.cpu().numpy() - ref) / scale).max() < 1e-5
 
 
@@ -236,8 +258,8 @@ def test_ess_depths_given_grid(dev, name):
 
 
 # ---------------------------------------------------------------- end to end
-def _render_fixture(dev, z):
-    pipe = _pipe(dev, z)
+def _render_fixture(dev, z, prec="fp32"):
+    pipe = _pipe(dev, z, mlp_precision=prec)
     pipe.set_weights(params_of(z))
     g = grid_of(z)
     if g is not None:
@@ -249,9 +271,10 @@ def _render_fixture(dev, z):
 
 
 @pytest.mark.parametrize("name", ALL)
-def test_render_coarse_maps_vs_golden(dev, name):
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_render_coarse_maps_vs_golden(dev, name, prec):
     z = load(name)
-    pipe, res = _render_fixture(dev, z)
+    pipe, res = _render_fixture(dev, z, prec)
     n = int(z["H"]) * int(z["W"])
     assert max_err(res["rgb_map_0"], z["out_rgb_map_0"].reshape(n, 3)) < TOL
     assert max_err(res["acc_map_0"], z["out_acc_map_0"].reshape(n)) < TOL
@@ -264,21 +287,23 @@ def test_render_coarse_maps_vs_golden(dev, name):
 
 
 @pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5")])
-def test_render_fine_maps_psnr_vs_golden(dev, name):
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_render_fine_maps_psnr_vs_golden(dev, name, prec):
     z = load(name)
-    _, res = _render_fixture(dev, z)
+    _, res = _render_fixture(dev, z, prec)
     n = int(z["H"]) * int(z["W"])
     assert psnr(res["rgb_map"], z["out_rgb_map"].reshape(n, 3)) > 35.0
 
 
 @pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5") and "ert" not in n])
-def test_fine_pass_given_reference_depths(dev, name):
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_fine_pass_given_reference_depths(dev, name, prec):
     """Fine MLP + composite on the reference's own fine depths: 1e-5."""
     z = load(name)
     zall = z["int_zall"]
     n, S2 = zall.shape
     oro, ord_ = O.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
-    pipe = _pipe(dev, z)
+    pipe = _pipe(dev, z, mlp_precision=prec)
     pipe.set_weights(params_of(z))
     ro, rd = _t(oro[:n], dev), _t(ord_[:n], dev)
     zt = _t(zall, dev)

@@ -17,7 +17,19 @@ PKG = os.path.join(REPO, "nerf-rep_for_test_amd")
 OUT = os.path.join(PKG, "build", "abl")
 VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"], "noenc": ["-DABL_NOENC"],
-            "noepi": ["-DABL_NOEPI"]}
+            "noepi": ["-DABL_NOEPI"],
+            # placement of the weight-DMA pieces (MLP_DMA_POS / EVERY / FIRST)
+            "pos1": ["-DMLP_DMA_POS=1"], "pos2": ["-DMLP_DMA_POS=2"], "pos3": ["-DMLP_DMA_POS=3"],
+            "ev4": ["-DMLP_DMA_EVERY=4", "-DMLP_DMA_FIRST=1"],
+            "ev4pos2": ["-DMLP_DMA_EVERY=4", "-DMLP_DMA_FIRST=1", "-DMLP_DMA_POS=2"],
+            "ev3pos2": ["-DMLP_DMA_EVERY=3", "-DMLP_DMA_FIRST=2", "-DMLP_DMA_POS=2"],
+            # the 3-term FP16 split kernel (mlp_x3.hip) and its ablations
+            "x3": [], "x3_nodma": ["-DABL_NODMA"], "x3_nobar": ["-DABL_NOBAR"],
+            "x3_nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"]}
+
+
+def is_x3(v):
+    return v.startswith("x3")
 FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-shared"]
 
@@ -25,8 +37,9 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=o
 def build(names):
     os.makedirs(OUT, exist_ok=True)
     for v in names:
+        src = "mlp_x3.hip" if is_x3(v) else "mlp_fused.hip"
         cmd = ["/opt/rocm/bin/hipcc", *FLAGS, *VARIANTS[v], os.path.join(PKG, "csrc", "runtime.hip"),
-               os.path.join(PKG, "csrc", "mlp_fused.hip"), "-o", os.path.join(OUT, f"lib_{v}.so")]
+               os.path.join(PKG, "csrc", src), "-o", os.path.join(OUT, f"lib_{v}.so")]
         subprocess.check_call(cmd)
         print("built", v)
 
@@ -35,11 +48,14 @@ def run(names, rounds, n_rays, S):
     sys.path.insert(0, PKG)
     import numpy as np
     import torch
-    from nerfhip.pack import pack_mlp
+    from nerfhip.pack import pack_mlp, pack_mlp_x3
     from nerfhip.synthetic import make_params
     dev = torch.device("cuda:0")
-    sl, hd = pack_mlp(make_params(0, 2.0, 0.0), "model")
-    sl, hd = torch.from_numpy(sl).to(dev), torch.from_numpy(hd).to(dev)
+    params = make_params(0, 2.0, 0.0)
+    packed = {}
+    for x3, fn in ((False, pack_mlp), (True, pack_mlp_x3)):
+        a, b = fn(params, "model")
+        packed[x3] = (torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev))
     g = torch.Generator().manual_seed(0)
     ro = (torch.rand((n_rays, 3), generator=g) * 0.2 + torch.tensor([0.0, 2.7, 3.0])).to(dev)
     rd = torch.nn.functional.normalize(torch.randn((n_rays, 3), generator=g), dim=1).to(dev)
@@ -48,18 +64,19 @@ def run(names, rounds, n_rays, S):
     libs = {}
     for v in names:
         h = ctypes.CDLL(os.path.join(OUT, f"lib_{v}.so"))
-        h.nerf_mlp_forward.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int64,
-                                                               ctypes.c_int, ctypes.c_void_p,
-                                                               ctypes.c_void_p]
-        libs[v] = h
+        fn = h.nerf_mlp_forward_x3 if is_x3(v) else h.nerf_mlp_forward
+        fn.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_void_p]
+        libs[v] = fn
     stream = torch.cuda.current_stream().cuda_stream
     times = {v: [] for v in names}
     for r in range(rounds + 1):
         for v in names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = libs[v].nerf_mlp_forward(sl.data_ptr(), hd.data_ptr(), ro.data_ptr(), rd.data_ptr(),
-                                          z.data_ptr(), 0, n_rays, S, raw.data_ptr(), stream)
+            sl, hd = packed[is_x3(v)]
+            rc = libs[v](sl.data_ptr(), hd.data_ptr(), ro.data_ptr(), rd.data_ptr(),
+                         z.data_ptr(), 0, n_rays, S, raw.data_ptr(), stream)
             e1.record()
             assert rc == 0, (v, rc)
             torch.cuda.synchronize()

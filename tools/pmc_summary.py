@@ -19,7 +19,7 @@ import json
 import os
 from collections import defaultdict
 
-SHORT = {"mlp_fused_kernel": "mlp_fused", "composite_kernel": "composite",
+SHORT = {"mlp_fused_kernel": "mlp_fused", "mlp_x3_kernel": "mlp_x3", "composite_kernel": "composite",
          "composite_ert_kernel": "composite_ert", "sample_fine_kernel": "sample_fine",
          "rays_kernel": "rays", "coarse_kernel": "coarse", "ess_kernel": "ess",
          "grid_update_kernel": "grid_update"}
