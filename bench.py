@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
                     help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
                          "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
+    ap.add_argument("--checkpoint", default=None,
+                    help="trained weights (a reference-format .pth or model dir) instead of "
+                         "the synthetic generator")
     ap.add_argument("--no-fp32-run", action="store_true",
                     help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
     args = ap.parse_args()
@@ -80,7 +83,13 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     H, W = args.H, args.W
-    params = make_params(0, 2.0, 0.0)
+    if args.checkpoint:
+        from nerfhip.checkpoint import network_params
+        params = {k: v.numpy() for k, v in network_params(args.checkpoint).items()}
+        data = f"checkpoint {args.checkpoint}, lego test cameras"
+    else:
+        params = make_params(0, 2.0, 0.0)
+        data = "synthetic weights (deterministic generator, seed 0, gain 2), lego test cameras"
 
     def barrier():
         if world > 1:
@@ -131,7 +140,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": DTYPES[args.precision],
-        "data": "synthetic weights (deterministic generator, seed 0, gain 2), lego test cameras",
+        "data": data,
         "config": {"workload": "lego 800x800, 64 coarse + 128 fine samples, 1 frame per step "
                                "(test poses cycled), ESS/ERT off, perturb 0, eval",
                    "H": H, "W": W, "N_samples": 64, "N_importance": 128,

@@ -81,7 +81,7 @@ __device__ __forceinline__ void run_group(Acc& acc, unsigned base, const BV& bv,
     constexpr int kPiece = (G - MLP_DMA_FIRST) / MLP_DMA_EVERY;
     auto piece = [&]() {
       if constexpr (kDma) {
-        if (dma.src) stage_piece(dma.src, dma.dst, dma.wave, dma.lane, kPiece);
+        if (dma.live) stage_piece<kPiece>(dma);
       }
     };
     lds_drain();
@@ -224,8 +224,7 @@ __global__ __launch_bounds__(kThreads, 2) void mlp_fused_kernel(
 
   // prologue: slices 0, 1, 2 in flight; slice 3 is staged while slice 0 runs
   for (int t = 0; t < 3; ++t)
-    for (int j = 0; j < kBlocksPerWave; ++j)
-      stage_piece(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane, j);
+    stage_slice(make_dma(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane));
   for (int i = tid; i < kHeadFloats / 4; i += kThreads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 

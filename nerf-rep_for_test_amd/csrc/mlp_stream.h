@@ -33,22 +33,39 @@ constexpr int kHeadScales = 3080;     // mlp_x3: per-layer weight scale exponent
 // ABL_NODMA the weight staging, ABL_NOENC the sin/cos, ABL_NOEPI the bias/ReLU.
 // One 1-KiB LDS-DMA piece (of the 4 each wave stages per slice): block
 // wave*4 + j of slice `src` into the same block of LDS buffer `dst`.
-__device__ __forceinline__ void stage_piece(const float4* src, float* dst, int wave, int lane,
-                                            int j) {
+// The piece index J is the instruction's immediate offset, which applies to the
+// global and the LDS address alike: a wave's 4 pieces of a slice share one
+// address VGPR pair and one M0 value.
+// DMA of one future slice by one wave, spread over the MFMA groups of the
+// current one: this lane's source (block wave*4 of the slice) and the wave's
+// LDS destination; live is false when there is no slice left to stage.
+struct Dma {
+  const float4* src;
+  float* dst;
+  int wave;
+  bool live;   // wave-uniform: a slice is left to stage
+};
+
+__device__ __forceinline__ Dma make_dma(const float4* slice, float* buf, int wave, int lane) {
+  const int b = wave * kBlocksPerWave;
+  return Dma{slice + b * 64 + lane, buf + b * 256, wave, slice != nullptr};
+}
+
+template <int J>
+__device__ __forceinline__ void stage_piece(const Dma& d) {
 #if defined(ABL_NODMA)
   return;
 #endif
-  const int b = wave * kBlocksPerWave + j;
-  __builtin_amdgcn_global_load_lds((const void*)(src + b * 64 + lane),
-                                   (lds_ptr_t)(dst + b * 256), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((const void*)d.src, (lds_ptr_t)d.dst, 16, J * 1024, 0);
 }
 
-// DMA of one future slice, spread over the MFMA groups of the current one.
-struct Dma {
-  const float4* src;   // slice in HBM/L2, or nullptr when there is none to stage
-  float* dst;          // its LDS ring buffer
-  int wave, lane;
-};
+// all 4 pieces of a slice (prologue)
+__device__ __forceinline__ void stage_slice(const Dma& d) {
+  stage_piece<0>(d);
+  stage_piece<1>(d);
+  stage_piece<2>(d);
+  stage_piece<3>(d);
+}
 
 // LDS fragment reads are issued as inline asm: hipcc neither tracks nor waits
 // for them, so the schedule below owns every lgkmcnt wait of the slice loop
@@ -84,8 +101,8 @@ struct Ring {
   __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
   __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
     const int t = g + 3;
-    return Dma{t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t), wave,
-               lane};
+    return make_dma(t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t),
+                    wave, lane);
   }
 };
 

@@ -18,7 +18,8 @@
 // 8 waves x 16 samples, 73 slices of 32 KiB; a slice of a 256-row layer holds
 // one 32-deep K step as 16 tiles x (hi, lo) fragment blocks (block 2m + part);
 // the views layer packs two K steps per slice (block 16q + 2m + part) and the
-// direction step alone in the last slice.
+// direction step alone in the last slice; the skip layer streams its 8
+// activation K steps before its 2 encoding K steps.
 //
 // Register dataflow: the accumulator of tile m holds, on lane l, sample l&15
 // and rows 16m + 4(l>>4) + r. K step q of the next layer takes, on lane group
@@ -29,16 +30,29 @@
 namespace nerfhip {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 
-struct Split {   // B operand of one K step: FP16 hi and lo parts
-  half8 h, l;
-};
+// B operand of one K step in 8 VGPRs: the 8 FP32 activations before the split,
+// the FP16 hi halves (VGPRs 0-3) and lo halves (VGPRs 4-7) after it.
+typedef f32x8 Op;
 
 constexpr int kX3Threads = 64 * kStreamWaves;
 constexpr int kX3Tile = 16 * kStreamWaves;
 
+#ifndef MLP_X3_STAGGER
+#define MLP_X3_STAGGER 0
+#endif
+
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ half8 op_hi(const Op& v) {
+  return __builtin_bit_cast(half8, __builtin_shufflevector(v, v, 0, 1, 2, 3));
+}
+__device__ __forceinline__ half8 op_lo(const Op& v) {
+  return __builtin_bit_cast(half8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+}
 
 template <int BLOCK>
 __device__ __forceinline__ half8 frag16(unsigned base) {
@@ -53,27 +67,39 @@ struct Frags {   // one group's A fragments: tiles m, m+1 x (hi, lo)
 
 template <int G>
 __device__ __forceinline__ void load_frags(Frags& f, unsigned base) {
+#if defined(ABL_HALFLDS)   // timing only: half the fragment reads (lo := hi)
+  f.h0 = frag16<4 * G + 0>(base);
+  f.h1 = frag16<4 * G + 2>(base);
+  f.l0 = f.h0;
+  f.l1 = f.h1;
+#else
   f.h0 = frag16<4 * G + 0>(base);
   f.l0 = frag16<4 * G + 1>(base);
   f.h1 = frag16<4 * G + 2>(base);
   f.l1 = frag16<4 * G + 3>(base);
+#endif
 }
 
-__device__ __forceinline__ void mfma3x2(f32x4& c0, f32x4& c1, const Frags& a, const Split& b) {
-  c0 = MFMA16(a.h0, b.h, c0);
-  c1 = MFMA16(a.h1, b.h, c1);
-  c0 = MFMA16(a.h0, b.l, c0);
-  c1 = MFMA16(a.h1, b.l, c1);
-  c0 = MFMA16(a.l0, b.h, c0);
-  c1 = MFMA16(a.l1, b.h, c1);
+// FIRST: the layer's first K step starts the accumulators from zero (no
+// clearing pass over them between layers).
+template <bool FIRST>
+__device__ __forceinline__ void mfma3x2(f32x4& c0, f32x4& c1, const Frags& a, const Op& b) {
+  const half8 bh = op_hi(b), bl = op_lo(b);
+  c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
+  c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
+  c0 = MFMA16(a.h0, bl, c0);
+  c1 = MFMA16(a.h1, bl, c1);
+  c0 = MFMA16(a.l0, bh, c0);
+  c1 = MFMA16(a.l1, bh, c1);
 }
 
 // Group G of NG: drain its fragment reads (issued one group earlier), issue
-// group G+1's into the other register set, 6 MFMAs, then (every other group)
-// one LDS-DMA piece of the slice three ahead.
-template <int G, int NG, typename Cfg, typename Acc, typename BV>
+// group G+1's into the other register set, 6 MFMAs, one LDS-DMA piece of the
+// slice three ahead (every other group), then the slice's hook for group G:
+// VALU work that fills the MFMA shadows (epilogue / operand split, below).
+template <int G, int NG, typename Cfg, typename Acc, typename BV, typename Hook>
 __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv, Frags& x,
-                                           Frags& y, const Dma& dma) {
+                                           Frags& y, const Dma& dma, Hook& hook) {
   if constexpr (G < NG) {
     lds_drain();
     if constexpr (G + 1 < NG) {
@@ -82,45 +108,51 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv
     }
     __builtin_amdgcn_sched_barrier(0);
     constexpr int m = Cfg::tile(G);
-    if constexpr ((G & 1) == 0) mfma3x2(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
-    else mfma3x2(acc[m], acc[m + 1], y, bv[Cfg::bsel(G)]);
+    if constexpr ((G & 1) == 0) mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
+    else mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], y, bv[Cfg::bsel(G)]);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((G & 1) == 0 && G / 2 < kBlocksPerWave) {
-      if (dma.src) stage_piece(dma.src, dma.dst, dma.wave, dma.lane, G / 2);
+#if MLP_X3_STAGGER
+    if constexpr (G / 2 < kBlocksPerWave) {
+      if (dma.live && (G & 1) == (dma.wave >> 2)) stage_piece<G / 2>(dma);
     }
+#else
+    if constexpr ((G & 1) == 0 && G / 2 < kBlocksPerWave) {
+      if (dma.live) stage_piece<G / 2>(dma);
+    }
+#endif
+    hook.template after<G>(acc);
     __builtin_amdgcn_sched_barrier(0);
-    run_group3<G + 1, NG, Cfg>(acc, base, bv, x, y, dma);
+    run_group3<G + 1, NG, Cfg>(acc, base, bv, x, y, dma, hook);
   }
 }
 
-template <int NG, typename Cfg, typename Acc, typename BV>
+template <int NG, typename Cfg, typename Acc, typename BV, typename Hook>
 __device__ __forceinline__ void run_slice3(Acc& acc, const float* buf, int lane, const BV& bv,
-                                           const Dma& dma) {
+                                           const Dma& dma, Hook& hook) {
   const unsigned base = lds_base(buf, lane);
   Frags x, y;
   load_frags<0>(x, base);
   y = x;
-  run_group3<0, NG, Cfg>(acc, base, bv, x, y, dma);
+  run_group3<0, NG, Cfg>(acc, base, bv, x, y, dma, hook);
 }
 
+// Slice shapes: the tiles, the B operand and whether the group starts its
+// tiles from zero (F: the layer's first slice; each tile only once).
 // 256-row layer slice = one K step (operand Q): groups G -> tiles 2G, 2G+1.
-template <int Q>
+template <int Q, bool F = false>
 struct Step256 {
+  static constexpr bool first(int) { return F; }
   static constexpr int tile(int g) { return 2 * g; }
   static constexpr int bsel(int) { return Q; }
 };
-// views slices = two K steps (operands Q0, Q0+1) x 8 tiles.
-template <int Q0>
+// views slices = two K steps (operands Q0, Q0+1) x 8 tiles: groups 4-7
+// revisit the tiles of groups 0-3 with the second K step.
+template <int Q0, bool F = false>
 struct StepViews {
+  static constexpr bool first(int g) { return F && g < 4; }
   static constexpr int tile(int g) { return 2 * (g & 3); }
   static constexpr int bsel(int g) { return Q0 + (g >> 2); }
 };
-
-template <int Q, typename BV>
-__device__ __forceinline__ void step256(f32x4 (&acc)[16], const float* buf, const BV& b, int lane,
-                                        const Dma& dma) {
-  run_slice3<8, Step256<Q>>(acc, buf, lane, b, dma);
-}
 
 // ---------------------------------------------------------------------------
 // activations: scale, FP16 split, B operands
@@ -139,82 +171,135 @@ __device__ __forceinline__ int act_exponent(float mx) {
   return 14 - E;
 }
 
-__device__ __forceinline__ void split8(const float (&v)[8], float s, Split& out) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float x = v[j] * s;
-    const _Float16 h = (_Float16)x;
-    out.h[j] = h;
-    out.l[j] = (_Float16)(x - (float)h);
-  }
+// FP16 hi/lo of two scaled values, packed: (hi pair, lo pair) as two dwords
+__device__ __forceinline__ void split2(float a, float b, float s, float& hp, float& lp) {
+#if defined(ABL_NOEPI)   // timing only
+  hp = __builtin_bit_cast(float, half2_t{(_Float16)a, (_Float16)b});
+  lp = hp;
+  (void)s;
+#else
+  // hi = f16(a*s), lo = f16(a*s - hi): one mixed-precision fma each (a*s is
+  // exact: s is a power of two)
+  const _Float16 ha = (_Float16)(a * s), hb = (_Float16)(b * s);
+  const half2_t h{ha, hb};
+  const half2_t l{(_Float16)__builtin_fmaf(a, s, -(float)ha),
+                  (_Float16)__builtin_fmaf(b, s, -(float)hb)};
+  hp = __builtin_bit_cast(float, h);
+  lp = __builtin_bit_cast(float, l);
+#endif
 }
 
-// B operands of the 8 K steps of a 256-wide activation held in tiles
-template <int Q>
-__device__ __forceinline__ void act_operands(const f32x4 (&a)[16], float s, Split (&X)[Q]) {
+__device__ __forceinline__ void split_op(Op& v, float s) {
+  Op o;
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = a[2 * q][j];
-      v[4 + j] = a[2 * q + 1][j];
+  for (int k = 0; k < 4; ++k) {
+    float hp, lp;
+    split2(v[2 * k], v[2 * k + 1], s, hp, lp);
+    o[k] = hp;
+    o[4 + k] = lp;
+  }
+  v = o;
+}
+
+struct NoHook {
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc&) {}
+};
+
+// Splits operand `op` (FP32 -> FP16 hi/lo at scale s) across the slice's even
+// groups: values 2k, 2k+1 after group 2k into a temporary, committed after the
+// last group (the operand is not read by this slice).
+struct SplitHook {
+  Op& op;
+  float s;
+  Op t;
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc&) {
+    if constexpr ((G & 1) == 0 && G < 8) {
+      float hp, lp;
+      split2(op[G], op[G + 1], s, hp, lp);
+      t[G / 2] = hp;
+      t[4 + G / 2] = lp;
     }
-    split8(v, s, X[q]);
+    if constexpr (G == 7) op = t;
   }
-}
+};
 
-template <int T>
-__device__ __forceinline__ float tiles_absmax(const f32x4 (&a)[T]) {
-  float m = 0.0f;
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) m = fmaxf(m, fabsf(a[t][r]));
-  return m;
-}
+// two operand splits in one slice (views layer)
+struct Split2 {
+  SplitHook a, b;
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    a.template after<G>(acc);
+    b.template after<G>(acc);
+  }
+};
 
-// acc * 2^-(sw + e) + bias (+ ReLU), in place: the layer's FP32 activations.
-// The power-of-two product is exact, so one fma rounds exactly like the
-// reference's separate add; ReLU is a max against a uniform floor (0, or
-// -inf for the feature layer) instead of a per-value select.
-template <int T>
-__device__ __forceinline__ void epilogue(f32x4 (&acc)[T], int shift, const float* bias, bool relu) {
-  const float inv = ldexpf(1.0f, -shift);
-  const float floor = relu ? 0.0f : -__builtin_inff();
+// Epilogue of a 256-row layer fused into its last slice (the K step that reads
+// operand 7 only): after group G, tiles 2G, 2G+1 are final -> acc * 2^-shift +
+// bias, ReLU floor, into operand X[G] as FP32 (split later); running |max|;
+// density-head partial dot (layer 7). The next layer's first slice restarts the
+// accumulators from zero.
+// The power-of-two product is exact, so the fma rounds like the reference's add.
+struct EpiHook {
+  Op (&X)[8];
+  float inv, floor;
+  const float* bias;   // lane-group packed [4m + r]
+  const float* aw;     // density-head weights (layer 7) or nullptr
+  float amax, apart;
+  bool on;             // false: the layer continues after this slice
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    if constexpr (G < 8) {
+      if (!on) return;
+      Op v;
 #pragma unroll
-  for (int m = 0; m < T; ++m)
+      for (int r = 0; r < 4; ++r) {
+#if defined(ABL_NOEPI)
+        v[r] = acc[2 * G][r];
+        v[4 + r] = acc[2 * G + 1][r];
+#else
+        v[r] = fmaxf(__builtin_fmaf(acc[2 * G][r], inv, bias[8 * G + r]), floor);
+        v[4 + r] = fmaxf(__builtin_fmaf(acc[2 * G + 1][r], inv, bias[8 * G + 4 + r]), floor);
+#endif
+      }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      acc[m][r] = fmaxf(__builtin_fmaf(acc[m][r], inv, bias[4 * m + r]), floor);
-}
+      for (int j = 0; j < 8; j += 2) amax = fmaxf(amax, fmaxf(fabsf(v[j]), fabsf(v[j + 1])));
+      if (aw) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) apart = __builtin_fmaf(v[j], aw[8 * G + j], apart);
+      }
+      X[G] = v;
+    }
+  }
+};
 
 // Frequency encoding of xyz (L=10) in this kernel's K order, lane group g:
 // slot i = 8q + j (q = 0, 1) holds sin (i even) / cos (i odd) of pair
 // 8g + i/2 = (band f, coordinate c) = divmod(pair, 3), for pairs < 30; lane
 // group 3 ends with x, y, z, 0 in slots 12..15.
-__device__ __forceinline__ void encode_xyz(const float (&p)[3], int g, float (&e)[16]) {
+__device__ __forceinline__ void encode_xyz(const float (&p)[3], int g, Op (&e)[2]) {
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int pr = 8 * g + t;
+    float a, b;
     if (pr < 30) {
       const int f = pr / 3, c = pr - 3 * f;
       const float x = c == 0 ? p[0] : (c == 1 ? p[1] : p[2]);
       const float arg = x * (float)(1 << f);   // exact power of two (freq.py:19)
-      float sv, cv;
-      sincosf(arg, &sv, &cv);
-      e[2 * t] = sv;
-      e[2 * t + 1] = cv;
+      sincosf(arg, &a, &b);
     } else {
-      e[2 * t] = t == 6 ? p[0] : (t == 7 ? p[2] : 0.0f);
-      e[2 * t + 1] = t == 6 ? p[1] : 0.0f;
+      a = t == 6 ? p[0] : (t == 7 ? p[2] : 0.0f);
+      b = t == 6 ? p[1] : 0.0f;
     }
+    e[t >> 2][(2 * t) & 7] = a;
+    e[t >> 2][(2 * t + 1) & 7] = b;
   }
 }
 
 // view-direction encoding (L=4): slots j = 2t, 2t+1 = sin, cos of (band g,
 // coordinate t), t < 3; slot 6 = raw coordinate g (g < 3); slot 7 = 0.
-__device__ __forceinline__ void encode_dir(const float (&d)[3], int g, float (&e)[8]) {
+__device__ __forceinline__ void encode_dir(const float (&d)[3], int g, Op& e) {
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const float arg = d[t] * (float)(1 << g);
@@ -227,14 +312,40 @@ __device__ __forceinline__ void encode_dir(const float (&d)[3], int g, float (&e
   e[7] = 0.0f;
 }
 
-__device__ __forceinline__ float absmax8(const float* v, int n) {
+__device__ __forceinline__ float op_absmax(const Op& v) {
   float m = 0.0f;
-  for (int i = 0; i < n; ++i) m = fmaxf(m, fabsf(v[i]));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
   return m;
 }
 
-__device__ __forceinline__ void zero(f32x4* a, int n) {
-  for (int m = 0; m < n; ++m) a[m] = f32x4(0.0f);
+// One 256-row slice (K step Q of operand array B) + its end-of-slice sync.
+template <int Q, bool FIRST, typename BV, typename Hook>
+__device__ __forceinline__ void slice256x(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
+                                          Hook& hook) {
+  run_slice3<8, Step256<Q, FIRST>>(acc, R.buf(g), R.lane, b, R.dma_for(g), hook);
+  slice_end<2>();
+}
+template <int Q, typename BV, typename Hook>
+__device__ __forceinline__ void slice256(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
+                                         Hook& hook) {
+  slice256x<Q, false>(acc, R, g, b, hook);
+}
+
+// The 8 activation slices g .. g+7 of a layer: the first restarts the
+// accumulators, slice q splits operand q+1 (scale s) in its MFMA shadows, the
+// last runs the fused epilogue (disabled for the skip layer, whose two
+// encoding slices follow).
+__device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int g, Op (&X)[8],
+                                           float s, EpiHook& epi) {
+  { SplitHook h{X[1], s}; slice256x<0, true>(acc, R, g + 0, X, h); }
+  { SplitHook h{X[2], s}; slice256<1>(acc, R, g + 1, X, h); }
+  { SplitHook h{X[3], s}; slice256<2>(acc, R, g + 2, X, h); }
+  { SplitHook h{X[4], s}; slice256<3>(acc, R, g + 3, X, h); }
+  { SplitHook h{X[5], s}; slice256<4>(acc, R, g + 4, X, h); }
+  { SplitHook h{X[6], s}; slice256<5>(acc, R, g + 5, X, h); }
+  { SplitHook h{X[7], s}; slice256<6>(acc, R, g + 6, X, h); }
+  slice256<7>(acc, R, g + 7, X, epi);
 }
 
 __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
@@ -252,8 +363,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const Ring R{ring, slices, wave, lane};
 
   for (int t = 0; t < 3; ++t)
-    for (int j = 0; j < kBlocksPerWave; ++j)
-      stage_piece(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane, j);
+    stage_slice(make_dma(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
@@ -269,82 +379,100 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     dv[c] = rays_d[ray * 3 + c];
     p[c] = rays_o[ray * 3 + c] + dv[c] * zv;      // VR:165: o + d*z, two roundings
   }
-  float encf[16];
+  Op encf[2];                   // FP32 encoding (split in place for the skip layer)
   encode_xyz(p, g4, encf);
-  const float enc_max = sample_max(absmax8(encf, 16));
+  const float enc_max = sample_max(fmaxf(op_absmax(encf[0]), op_absmax(encf[1])));
 
-  f32x4 acc[16];
-  Split X[8];
-  Split E[2];
+  f32x4 acc[16];   // every layer's first slice starts it from zero
+  Op X[8];
   __syncthreads();   // head, z/rays loads and the three prologue slices resident
 
-  // ---- layer 0: 63 -> 256 (slices 0, 1) ------------------------------------
+  // ---- layer 0: 63 -> 256 (slices 0, 1), epilogue fused into slice 1 --------
   int e = act_exponent(enc_max);
+  float s = ldexpf(1.0f, e);
   {
-    const float s = ldexpf(1.0f, e);
-    split8(*reinterpret_cast<const float(*)[8]>(&encf[0]), s, E[0]);
-    split8(*reinterpret_cast<const float(*)[8]>(&encf[8]), s, E[1]);
+    Op E[2] = {encf[0], encf[1]};   // split copy: the FP32 encoding returns at layer 5
+    split_op(E[0], s);
+    split_op(E[1], s);
+    NoHook nh;
+    slice256x<0, true>(acc, R, 0, E, nh);
+    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 0] + e)), 0.0f,
+                hd + kHeadBias + g4 * 64, nullptr, 0.0f, 0.0f, true};
+    slice256<1>(acc, R, 1, E, epi);
+    e = act_exponent(sample_max(epi.amax));
   }
-  zero(acc, 16);
-  step256<0>(acc, R.buf(0), E, lane, R.dma_for(0)); slice_end<2>();
-  step256<1>(acc, R.buf(1), E, lane, R.dma_for(1)); slice_end<2>();
-  epilogue(acc, (int)hd[kHeadScales + 0] + e, hd + kHeadBias + g4 * 64, true);
+  s = ldexpf(1.0f, e);
+  split_op(X[0], s);
   int g = 2;
 
   float alpha = 0.0f;
+  // ---- layers 1..7 (skip input at 5) + feature (8, no ReLU) ----------------
   for (int L = 1; L <= 8; ++L) {
-    // scale of this layer's input (the skip layer shares it with the encoding)
-    float mx = tiles_absmax(acc);
-    if (L == 5) mx = fmaxf(mx, enc_max);
-    e = act_exponent(sample_max(mx));
-    const float s = ldexpf(1.0f, e);
-    act_operands(acc, s, X);
-    zero(acc, 16);
-    if (L == 5) {   // cat(input_pts, h): the encoded input first (NET:57-58)
-      split8(*reinterpret_cast<const float(*)[8]>(&encf[0]), s, E[0]);
-      split8(*reinterpret_cast<const float(*)[8]>(&encf[8]), s, E[1]);
-      step256<0>(acc, R.buf(g), E, lane, R.dma_for(g)); slice_end<2>();
-      step256<1>(acc, R.buf(g + 1), E, lane, R.dma_for(g + 1)); slice_end<2>();
-      g += 2;
-    }
-    step256<0>(acc, R.buf(g + 0), X, lane, R.dma_for(g + 0)); slice_end<2>();
-    step256<1>(acc, R.buf(g + 1), X, lane, R.dma_for(g + 1)); slice_end<2>();
-    step256<2>(acc, R.buf(g + 2), X, lane, R.dma_for(g + 2)); slice_end<2>();
-    step256<3>(acc, R.buf(g + 3), X, lane, R.dma_for(g + 3)); slice_end<2>();
-    step256<4>(acc, R.buf(g + 4), X, lane, R.dma_for(g + 4)); slice_end<2>();
-    step256<5>(acc, R.buf(g + 5), X, lane, R.dma_for(g + 5)); slice_end<2>();
-    step256<6>(acc, R.buf(g + 6), X, lane, R.dma_for(g + 6)); slice_end<2>();
-    step256<7>(acc, R.buf(g + 7), X, lane, R.dma_for(g + 7)); slice_end<2>();
+    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)),
+                L != 8 ? 0.0f : -__builtin_inff(), hd + kHeadBias + L * 256 + g4 * 64,
+                L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
+    act_slices(acc, R, g, X, s, epi);
     g += 8;
-    epilogue(acc, (int)hd[kHeadScales + L] + e, hd + kHeadBias + L * 256 + g4 * 64, L != 8);
-    if (L == 7) {   // density head on h (NET:61), FP32 on the VALU
-      const float* aw = hd + kHeadAlphaW + g4 * 64;
-      float part = 0.0f;
-#pragma unroll
-      for (int m = 0; m < 16; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) part = __builtin_fmaf(acc[m][r], aw[4 * m + r], part);
-      alpha = quad_sum(part) + hd[kHeadAlphaB];
+    if (L == 5) {   // cat(input_pts, h) (NET:57-58): the encoding's K steps last
+      NoHook nh;
+      slice256<0>(acc, R, g, encf, nh);
+      slice256<1>(acc, R, g + 1, encf, nh);
+      g += 2;
+      epi.on = true;   // this layer's epilogue, not pipelined
+      epi.after<0>(acc); epi.after<1>(acc); epi.after<2>(acc); epi.after<3>(acc);
+      epi.after<4>(acc); epi.after<5>(acc); epi.after<6>(acc); epi.after<7>(acc);
+    }
+    if (L == 7) alpha = quad_sum(epi.apart) + hd[kHeadAlphaB];   // NET:61
+    // the next layer's input scale (the skip layer's covers the encoding too)
+    float mx = epi.amax;
+    if (L == 4) mx = fmaxf(mx, enc_max);
+    if (L == 8) break;
+    e = act_exponent(sample_max(mx));
+    s = ldexpf(1.0f, e);
+    split_op(X[0], s);
+    if (L == 4) {   // the FP32 encoding is not needed after the skip layer
+      split_op(encf[0], s);
+      split_op(encf[1], s);
     }
   }
+  // acc holds zeros; X holds the feature layer (FP32, unsplit)
 
   // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67) -
-  float dirf[8];
+  Op dirf;
   encode_dir(dv, g4, dirf);
-  e = act_exponent(sample_max(fmaxf(tiles_absmax(acc), absmax8(dirf, 8))));
   {
-    const float s = ldexpf(1.0f, e);
-    act_operands(acc, s, X);
-    split8(dirf, s, E[0]);
+    float mx = op_absmax(dirf);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mx = fmaxf(mx, op_absmax(X[q]));
+    e = act_exponent(sample_max(mx));
   }
-  f32x4 acc8[8];
-  zero(acc8, 8);
-  run_slice3<8, StepViews<0>>(acc8, R.buf(g), lane, X, R.dma_for(g)); slice_end<2>();           // 68
-  run_slice3<8, StepViews<2>>(acc8, R.buf(g + 1), lane, X, R.dma_for(g + 1)); slice_end<2>();   // 69
-  run_slice3<8, StepViews<4>>(acc8, R.buf(g + 2), lane, X, R.dma_for(g + 2)); slice_end<1>();   // 70
-  run_slice3<8, StepViews<6>>(acc8, R.buf(g + 3), lane, X, R.dma_for(g + 3)); slice_end<0>();   // 71
-  run_slice3<4, Step256<0>>(acc8, R.buf(g + 4), lane, E, R.dma_for(g + 4));                     // 72
-  epilogue(acc8, (int)hd[kHeadScales + 9] + e, hd + kHeadBiasViews + g4 * 32, true);
+  s = ldexpf(1.0f, e);
+  split_op(X[0], s);
+  split_op(X[1], s);
+  f32x4 acc8[8];   // started from zero by the first views slice
+  {
+    // views slice k reads operands 2k, 2k+1 and splits 2k+2, 2k+3 (then dir)
+    Split2 h0{{X[2], s}, {X[3], s}};
+    run_slice3<8, StepViews<0, true>>(acc8, R.buf(g), lane, X, R.dma_for(g), h0); slice_end<2>();
+    Split2 h1{{X[4], s}, {X[5], s}};
+    run_slice3<8, StepViews<2>>(acc8, R.buf(g + 1), lane, X, R.dma_for(g + 1), h1); slice_end<2>();
+    Split2 h2{{X[6], s}, {X[7], s}};
+    run_slice3<8, StepViews<4>>(acc8, R.buf(g + 2), lane, X, R.dma_for(g + 2), h2); slice_end<1>();
+    SplitHook h3{dirf, s};
+    run_slice3<8, StepViews<6>>(acc8, R.buf(g + 3), lane, X, R.dma_for(g + 3), h3); slice_end<0>();
+    NoHook nh;
+    const Op D[1] = {dirf};
+    run_slice3<4, Step256<0>>(acc8, R.buf(g + 4), lane, D, R.dma_for(g + 4), nh);
+  }
+  {   // views epilogue (bias, ReLU) -- once per pass, not pipelined
+    const float inv = ldexpf(1.0f, -((int)hd[kHeadScales + 9] + e));
+    const float* bias = hd + kHeadBiasViews + g4 * 32;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc8[m][r] = fmaxf(__builtin_fmaf(acc8[m][r], inv, bias[4 * m + r]), 0.0f);
+  }
 
   // ---- rgb head (NET:68-70), FP32 on the VALU --------------------------------
   float part[3] = {0.0f, 0.0f, 0.0f};

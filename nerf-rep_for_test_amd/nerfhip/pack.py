@@ -281,8 +281,8 @@ def _x3_layer_cols(kind):
         return x3_cols_enc()
     if kind == "act":
         return act
-    if kind == "skip":
-        return np.concatenate([x3_cols_enc(), IN_XYZ + act], 0)
+    if kind == "skip":      # activation steps first, the encoding's last
+        return np.concatenate([IN_XYZ + act, x3_cols_enc()], 0)
     if kind == "views":
         d = x3_cols_dir()
         return np.concatenate([act, np.where(d >= 0, W + d, -1)], 0)
@@ -400,13 +400,12 @@ def emulate_x3(slices, head, pts, dirs):
             mx = np.maximum(mx, np.abs(enc_feat).max(1))
         e = exponent(mx)
         Xh, Xl = split(gather(x, ca), 2.0 ** e)
-        acc = np.zeros((256, P))
+        acc = mm(list(range(g, g + 8)), [0] * 8, Xh, Xl, 16)
+        g += 8
         if L == 5:
             Eh, El = split(gather(enc_feat, ce), 2.0 ** e)
             acc += mm([g, g + 1], [0, 0], Eh, El, 16)
             g += 2
-        acc += mm(list(range(g, g + 8)), [0] * 8, Xh, Xl, 16)
-        g += 8
         h = acc * 2.0 ** -(hd[H_SCALES + L] + e) + bias_of(H_BIAS + L * 256, 16)[:, None]
         if L != 8:
             h = np.maximum(h, 0)

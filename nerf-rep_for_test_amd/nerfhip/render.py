@@ -81,6 +81,11 @@ class NerfPipeline:
         self.coarse = up(coarse_prefix)
         self.fine = up(fine_prefix) if self.N_importance > 0 else None
 
+    def load_checkpoint(self, model_dir, epoch=-1):
+        """Weights from a checkpoint in the reference's format (nerfhip.checkpoint)."""
+        from .checkpoint import network_params
+        self.set_weights(network_params(model_dir, epoch))
+
     def set_grid(self, grid):
         g = torch.as_tensor(grid)
         self.grid_res = int(g.shape[0])

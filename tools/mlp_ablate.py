@@ -25,12 +25,15 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "ev3pos2": ["-DMLP_DMA_EVERY=3", "-DMLP_DMA_FIRST=2", "-DMLP_DMA_POS=2"],
             # the 3-term FP16 split kernel (mlp_x3.hip) and its ablations
             "x3": [], "x3_nodma": ["-DABL_NODMA"], "x3_nobar": ["-DABL_NOBAR"],
-            "x3_nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"]}
+            "x3_nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"],
+            "x3_stagger": ["-DMLP_X3_STAGGER=1"], "x3_halflds": ["-DABL_HALFLDS"],
+            "x3_halflds_nodma": ["-DABL_HALFLDS", "-DABL_NODMA"],
+            "x3_noepi": ["-DABL_NOEPI"]}
 
 
 def is_x3(v):
     return v.startswith("x3")
-FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off",
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off", "-fno-slp-vectorize",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-shared"]
 
 
