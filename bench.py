@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
                     help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
                          "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
+    ap.add_argument("--config", default="c2", choices=["c2", "c4"],
+                    help="c2: lego 800x800 64c+128f (BASELINE configs[1], the headline); "
+                         "c4: the same with ESS + ERT (configs[3], lego.yaml:96-99)")
     ap.add_argument("--checkpoint", default=None,
                     help="trained weights (a reference-format .pth or model dir) instead of "
                          "the synthetic generator")
@@ -69,7 +72,7 @@ def main():
     import torch.distributed as dist
     from nerfhip.dist import render_frame_sharded
     from nerfhip.render import NerfPipeline
-    from nerfhip.synthetic import make_params
+    from nerfhip.synthetic import make_occupancy_grid, make_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -95,17 +98,26 @@ def main():
         if world > 1:
             dist.barrier()
 
+    c4 = args.config == "c4"
+
+    def make_pipe(precision):
+        pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
+                            mlp_precision=precision, enable_ess=c4, enable_ert=c4,
+                            ert_threshold=0.01)
+        pipe.set_weights(params)
+        if c4:
+            pipe.set_grid(make_occupancy_grid(0, 128, 1.2, 0.1))
+        return pipe
+
     def measure(precision):
         """warmup + K timed frames (barrier + sync both sides, max over ranks)."""
-        pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
-                            mlp_precision=precision)
-        pipe.set_weights(params)
+        pipe = make_pipe(precision)
 
         def frame(i):
             pose, K = lego_camera(H, W, i)
             return render_frame_sharded(
                 lambda p0, n: pipe.render_image(H, W, pose, K, p0=p0, n=n),
-                H, W, rank, world, dev)
+                H, W, rank, world, dev, chunk_aligned=c4)
 
         for i in range(args.warmup):
             frame(i)
@@ -142,14 +154,22 @@ def main():
         "dtype": DTYPES[args.precision],
         "data": data,
         "config": {"workload": "lego 800x800, 64 coarse + 128 fine samples, 1 frame per step "
-                               "(test poses cycled), ESS/ERT off, perturb 0, eval",
+                               "(test poses cycled), " +
+                               ("ESS + ERT on (threshold 0.01, synthetic occupancy grid, "
+                                "2048-ray chunks)" if c4 else "ESS/ERT off") + ", perturb 0, eval",
+                   "baseline_config": "configs[3]" if c4 else "configs[1]",
                    "H": H, "W": W, "N_samples": 64, "N_importance": 128,
                    "mlp_precision": args.precision,
                    "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"], result["parity"] = cpu_baseline(pipe, H, W, params, args.cpu_rows)
+        if c4:
+            result["cpu_baseline"], result["parity"] = cpu_baseline_c4(
+                make_pipe(args.precision), H, W, params, args.cpu_rows)
+        else:
+            result["cpu_baseline"], result["parity"] = cpu_baseline(pipe, H, W, params,
+                                                                    args.cpu_rows)
         result["psnr_vs_ref"] = result["parity"]["psnr_fine_rgb"]
     del pipe
     if args.precision != "fp32" and not args.no_fp32_run:
@@ -216,11 +236,7 @@ def cpu_baseline(pipe, H, W, params, rows):
     sys.path.insert(0, REPO)
     from oracle import nerf_oracle as O
     import torch
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([t.get("num_threads", 1) for t in threadpool_info()] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    threads = _threads()
     pose, K = lego_camera(H, W, 0)
     r0 = max(0, H // 2 - rows // 2)
     ro, rd = O.camera_rays(H, W, pose, K)
@@ -233,24 +249,64 @@ def cpu_baseline(pipe, H, W, params, rows):
     torch.cuda.synchronize()
     g = {k: v.cpu().numpy() for k, v in gpu.items()}
     n = rows * W
-
-    def mx(a, b):
-        m = ~np.isnan(b)
-        return float(np.abs(a[m] - b[m]).max())
-
-    mse = float(np.mean((np.clip(g["rgb_map"], 0, 1) - np.clip(ref["rgb_map"].reshape(n, 3), 0, 1)) ** 2))
-    parity = {
-        "strip_rows": [r0, r0 + rows],
-        "max_abs_err_rgb_map_0": mx(g["rgb_map_0"], ref["rgb_map_0"].reshape(n, 3)),
-        "max_abs_err_depth_map_0": mx(g["depth_map_0"], ref["depth_map_0"].reshape(n)),
-        "max_abs_err_rgb_map": mx(g["rgb_map"], ref["rgb_map"].reshape(n, 3)),
-        "psnr_fine_rgb": (float("inf") if mse == 0 else -10 * np.log10(mse)),
-    }
+    parity = {"strip_rows": [r0, r0 + rows], **_parity(g, ref, n)}
     base = {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(threads),
             "kind": "port", "seconds": t_cpu,
             "sample": f"rows {r0}-{r0 + rows - 1} of lego test frame 0 at {H}x{W} "
                       f"({n} rays, 64c+128f) rendered by oracle/nerf_oracle.py (numpy float32)"}
     return base, parity
+
+
+def cpu_baseline_c4(pipe, H, W, params, rows):
+    """ESS + ERT: the oracle on the frame's first whole 2048-ray chunks (about
+    `rows` rows), fresh grid and call counter on both sides."""
+    sys.path.insert(0, REPO)
+    from oracle import nerf_oracle as O
+    from nerfhip.synthetic import make_occupancy_grid
+    import torch
+    threads = _threads()
+    pose, K = lego_camera(H, W, 0)
+    n = max(1, rows * W // 2048) * 2048
+    ro, rd = O.camera_rays(H, W, pose, K)
+    grid = make_occupancy_grid(0, 128, 1.2, 0.1)
+    cfg = O.RenderConfig(N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
+                         ert_threshold=0.01)
+    t0 = time.perf_counter()
+    ref, _ = O.render(1, n, pose, K, params, cfg, grid=grid.copy(), grid_counter=0,
+                      rays=(ro[:n], rd[:n]))
+    t_cpu = time.perf_counter() - t0
+    pipe.grid_update_counter = 0
+    gpu = pipe.render_image(H, W, pose, K, p0=0, n=n)
+    torch.cuda.synchronize()
+    g = {k: v.cpu().numpy() for k, v in gpu.items()}
+    parity = _parity(g, ref, n)
+    parity["rays"] = [0, n]
+    base = {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(threads), "kind": "port",
+            "seconds": t_cpu,
+            "sample": f"rays 0-{n - 1} ({n // 2048} whole 2048-ray chunks) of lego test frame 0 "
+                      f"at {H}x{W}, 64c+128f, ESS + ERT, rendered by oracle/nerf_oracle.py"}
+    return base, parity
+
+
+def _threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([t.get("num_threads", 1) for t in threadpool_info()] or [1])
+    except Exception:
+        return int(os.environ.get("OMP_NUM_THREADS", "1"))
+
+
+def _parity(g, ref, n):
+    def mx(a, b):
+        m = ~np.isnan(b)
+        return float(np.abs(a[m] - b[m]).max()) if m.any() else 0.0
+
+    mse = float(np.mean((np.clip(g["rgb_map"], 0, 1) -
+                         np.clip(ref["rgb_map"].reshape(n, 3), 0, 1)) ** 2))
+    return {"max_abs_err_rgb_map_0": mx(g["rgb_map_0"], ref["rgb_map_0"].reshape(n, 3)),
+            "max_abs_err_depth_map_0": mx(g["depth_map_0"], ref["depth_map_0"].reshape(n)),
+            "max_abs_err_rgb_map": mx(g["rgb_map"], ref["rgb_map"].reshape(n, 3)),
+            "psnr_fine_rgb": (float("inf") if mse == 0 else -10 * np.log10(mse))}
 
 
 if __name__ == "__main__":

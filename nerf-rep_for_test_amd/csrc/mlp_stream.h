@@ -43,12 +43,13 @@ struct Dma {
   const float4* src;
   float* dst;
   int wave;
-  bool live;   // wave-uniform: a slice is left to stage
+  int live;    // wave-uniform: a slice is left to stage
 };
 
 __device__ __forceinline__ Dma make_dma(const float4* slice, float* buf, int wave, int lane) {
   const int b = wave * kBlocksPerWave;
-  return Dma{slice + b * 64 + lane, buf + b * 256, wave, slice != nullptr};
+  return Dma{slice + b * 64 + lane, buf + b * 256, wave,
+             __builtin_amdgcn_readfirstlane(slice != nullptr ? 1 : 0)};
 }
 
 template <int J>

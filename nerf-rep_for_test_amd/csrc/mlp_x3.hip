@@ -47,6 +47,10 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(p);
+}
+
 __device__ __forceinline__ half8 op_hi(const Op& v) {
   return __builtin_bit_cast(half8, __builtin_shufflevector(v, v, 0, 1, 2, 3));
 }
@@ -106,6 +110,7 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv
       if constexpr ((G & 1) == 0) load_frags<G + 1>(y, base);
       else load_frags<G + 1>(x, base);
     }
+    hook.template prefetch<G>();   // the hook's own LDS reads, drained with the frags
     __builtin_amdgcn_sched_barrier(0);
     constexpr int m = Cfg::tile(G);
     if constexpr ((G & 1) == 0) mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
@@ -202,6 +207,8 @@ __device__ __forceinline__ void split_op(Op& v, float s) {
 }
 
 struct NoHook {
+  template <int G>
+  __device__ __forceinline__ void prefetch() {}
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc&) {}
 };
@@ -209,15 +216,20 @@ struct NoHook {
 // Splits operand `op` (FP32 -> FP16 hi/lo at scale s) across the slice's even
 // groups: values 2k, 2k+1 after group 2k into a temporary, committed after the
 // last group (the operand is not read by this slice).
+// The empty asm takes the results as register operands at this point of the
+// program, so IR-level sinking cannot move the work to the commit.
 struct SplitHook {
   Op& op;
   float s;
   Op t;
+  template <int G>
+  __device__ __forceinline__ void prefetch() {}
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc&) {
     if constexpr ((G & 1) == 0 && G < 8) {
       float hp, lp;
       split2(op[G], op[G + 1], s, hp, lp);
+      asm volatile("" : "+v"(hp), "+v"(lp));
       t[G / 2] = hp;
       t[4 + G / 2] = lp;
     }
@@ -228,6 +240,8 @@ struct SplitHook {
 // two operand splits in one slice (views layer)
 struct Split2 {
   SplitHook a, b;
+  template <int G>
+  __device__ __forceinline__ void prefetch() {}
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
     a.template after<G>(acc);
@@ -244,13 +258,32 @@ struct Split2 {
 struct EpiHook {
   Op (&X)[8];
   float inv, floor;
-  const float* bias;   // lane-group packed [4m + r]
+  unsigned bias;       // LDS byte address of this lane group's packed biases [4m + r]
   const float* aw;     // density-head weights (layer 7) or nullptr
   float amax, apart;
   bool on;             // false: the layer continues after this slice
+  f32x4 bb[2][2];      // biases of pairs G (G & 1), loaded in group G's read phase
+  template <int G>
+  __device__ __forceinline__ void prefetch() {
+    if constexpr (G < 8) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bb[G & 1][0]) : "v"(bias), "i"(32 * G) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bb[G & 1][1]) : "v"(bias), "i"(32 * G + 16) : "memory");
+    }
+  }
+  // in the slice: tile pair G-1 after group G (its MFMA results have landed
+  // while group G issued); pair 7 by finish() after the slice
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
-    if constexpr (G < 8) {
+    if constexpr (G >= 1 && G <= 8) pair<G - 1>(acc);
+  }
+  template <typename Acc>
+  __device__ __forceinline__ void finish(Acc& acc) {
+    lds_drain();   // pair 7's biases (read in group 7)
+    pair<7>(acc);
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void pair(Acc& acc) {
+    {
       if (!on) return;
       Op v;
 #pragma unroll
@@ -259,16 +292,18 @@ struct EpiHook {
         v[r] = acc[2 * G][r];
         v[4 + r] = acc[2 * G + 1][r];
 #else
-        v[r] = fmaxf(__builtin_fmaf(acc[2 * G][r], inv, bias[8 * G + r]), floor);
-        v[4 + r] = fmaxf(__builtin_fmaf(acc[2 * G + 1][r], inv, bias[8 * G + 4 + r]), floor);
+        v[r] = fmaxf(__builtin_fmaf(acc[2 * G][r], inv, bb[G & 1][0][r]), floor);
+        v[4 + r] = fmaxf(__builtin_fmaf(acc[2 * G + 1][r], inv, bb[G & 1][1][r]), floor);
 #endif
       }
 #pragma unroll
-      for (int j = 0; j < 8; j += 2) amax = fmaxf(amax, fmaxf(fabsf(v[j]), fabsf(v[j + 1])));
+      for (int j = 0; j < 8; j += 2)
+        asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(amax) : "v"(v[j]), "v"(v[j + 1]));
       if (aw) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) apart = __builtin_fmaf(v[j], aw[8 * G + j], apart);
       }
+      asm volatile("" : "+v"(v), "+v"(amax));   // computed here, not sunk to the use
       X[G] = v;
     }
   }
@@ -332,6 +367,17 @@ __device__ __forceinline__ void slice256(f32x4 (&acc)[16], const Ring& R, int g,
   slice256x<Q, false>(acc, R, g, b, hook);
 }
 
+// A whole epilogue outside a slice (skip layer): each pair's biases, then it.
+template <int P>
+__device__ __forceinline__ void epi_pairs(EpiHook& epi, f32x4 (&acc)[16]) {
+  if constexpr (P < 8) {
+    epi.prefetch<P>();
+    lds_drain();
+    epi.pair<P>(acc);
+    epi_pairs<P + 1>(epi, acc);
+  }
+}
+
 // The 8 activation slices g .. g+7 of a layer: the first restarts the
 // accumulators, slice q splits operand q+1 (scale s) in its MFMA shadows, the
 // last runs the fused epilogue (disabled for the skip layer, whose two
@@ -346,6 +392,7 @@ __device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int 
   { SplitHook h{X[6], s}; slice256<5>(acc, R, g + 5, X, h); }
   { SplitHook h{X[7], s}; slice256<6>(acc, R, g + 6, X, h); }
   slice256<7>(acc, R, g + 7, X, epi);
+  epi.finish(acc);
 }
 
 __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
@@ -397,8 +444,9 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     NoHook nh;
     slice256x<0, true>(acc, R, 0, E, nh);
     EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 0] + e)), 0.0f,
-                hd + kHeadBias + g4 * 64, nullptr, 0.0f, 0.0f, true};
+                lds_addr(hd + kHeadBias + g4 * 64), nullptr, 0.0f, 0.0f, true};
     slice256<1>(acc, R, 1, E, epi);
+    epi.finish(acc);
     e = act_exponent(sample_max(epi.amax));
   }
   s = ldexpf(1.0f, e);
@@ -409,7 +457,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   // ---- layers 1..7 (skip input at 5) + feature (8, no ReLU) ----------------
   for (int L = 1; L <= 8; ++L) {
     EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)),
-                L != 8 ? 0.0f : -__builtin_inff(), hd + kHeadBias + L * 256 + g4 * 64,
+                L != 8 ? 0.0f : -__builtin_inff(), lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
                 L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
     act_slices(acc, R, g, X, s, epi);
     g += 8;
@@ -419,8 +467,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
       slice256<1>(acc, R, g + 1, encf, nh);
       g += 2;
       epi.on = true;   // this layer's epilogue, not pipelined
-      epi.after<0>(acc); epi.after<1>(acc); epi.after<2>(acc); epi.after<3>(acc);
-      epi.after<4>(acc); epi.after<5>(acc); epi.after<6>(acc); epi.after<7>(acc);
+      epi_pairs<0>(epi, acc);
     }
     if (L == 7) alpha = quad_sum(epi.apart) + hd[kHeadAlphaB];   // NET:61
     // the next layer's input scale (the skip layer's covers the encoding too)
