@@ -58,9 +58,10 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
                     help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
                          "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"],
                     help="c2: lego 800x800 64c+128f (BASELINE configs[1], the headline); "
-                         "c4: the same with ESS + ERT (configs[3], lego.yaml:96-99)")
+                         "c3: train step, 1024 rays/rank (configs[2]); "
+                         "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99)")
     ap.add_argument("--checkpoint", default=None,
                     help="trained weights (a reference-format .pth or model dir) instead of "
                          "the synthetic generator")
@@ -99,6 +100,8 @@ def main():
             dist.barrier()
 
     c4 = args.config == "c4"
+    if args.config == "c3":
+        return bench_train(args, world, rank, dev, params, data, barrier)
 
     def make_pipe(precision):
         pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
@@ -176,6 +179,70 @@ def main():
         _, el32, roof32 = measure("fp32")
         result["fp32_mfma"] = {"value": rays / el32 / 1e6, "ms_per_step": el32 / args.steps * 1e3,
                                "dtype": DTYPES["fp32"], "roofline": roof32}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_train(args, world, rank, dev, params, data, barrier):
+    """C3: NerfTrainer.step on 1024 random lego-camera pixels per rank (synthetic
+    targets), data parallel over ranks (weak scaling)."""
+    import torch
+    import torch.distributed as dist
+    from nerfhip.render import NerfPipeline
+    from nerfhip.train import NerfTrainer, camera_rays_at
+    cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
+    H = W = 800
+    focal = 0.5 * W / np.tan(0.5 * float(cams["camera_angle_x"]))
+    poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
+    K = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32,
+                     device=dev)
+    tr = NerfTrainer(dev, params)
+    group = dist.group.WORLD if world > 1 else None
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    nrays = 1024
+
+    def batch():
+        pix = torch.randint(0, H * W, (nrays,), device=dev, generator=gen)
+        view = torch.randint(0, poses.shape[0], (nrays,), device=dev, generator=gen)
+        ro, rd = camera_rays_at(poses, K, pix, view, W)
+        target = torch.rand((nrays, 3), device=dev, generator=gen)
+        return ro, rd, target
+
+    batches = [batch() for _ in range(args.warmup + args.steps)]
+    for i in range(args.warmup):
+        tr.step(*batches[i], group=group)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        losses = tr.step(*batches[args.warmup + i], group=group)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_s = elapsed / args.steps
+    flop = 3 * NerfPipeline.MLP_FLOP_PER_SAMPLE * nrays * (64 + 192)   # fwd + 2x bwd
+    result = {
+        "metric": "train step: Mrays/s (1024 rays/rank/step, 64c+128f) + ms/step",
+        "value": nrays * world * args.steps / elapsed / 1e6, "unit": "Mrays/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": data + ", synthetic targets",
+        "config": {"workload": "lego train step: 1024 random pixels of the test cameras per "
+                               "rank, perturb 1, training-mode u, MSE coarse+fine, clip 40, Adam",
+                   "baseline_config": "configs[2]", "N_rays": nrays, "N_samples": 64,
+                   "N_importance": 128, "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
+        "roofline": {"bound": "mfma", "kernel": "whole step (MLP GEMMs on hipBLASLt dominate)",
+                     "achieved": flop / step_s / 1e12, "peak": FP32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": flop / step_s / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": None, "flop_per_step": flop},
+        "loss_last": float(losses["loss"].item()),
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

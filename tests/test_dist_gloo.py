@@ -76,3 +76,33 @@ def test_band_partition_covers_image():
                     assert p0 % nd.REF_CHUNK == 0
                 seen.extend(range(p0, p0 + n))
             assert seen == list(range(H * W))
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nerfhip.train import allreduce_mean
+        grads = [torch.full((3, 4), float(rank + 1)), torch.arange(5, dtype=torch.float32) * (rank + 1)]
+        allreduce_mean(grads, dist.group.WORLD)
+        q.put((rank, [g.numpy().copy() for g in grads]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_gradient_allreduce_mean():
+    """Data-parallel C3 step: every rank ends with the mean of the ranks' gradients."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        a, b = got[rank]
+        assert (a == 1.5).all()
+        assert (b == torch.arange(5).numpy() * 1.5).all()
