@@ -18,6 +18,7 @@ import torch
 
 from src.config import cfg
 from nerfhip import _lib
+from nerfhip.paths import spiral_poses
 from nerfhip.render import NerfPipeline
 
 
@@ -143,13 +144,38 @@ class Renderer:
 
     # ------------------------------------------------------------- paths
     def generate_spiral_poses(self, poses, n_frames=None, n_rots=2, zrate=0.5):
-        raise NotImplementedError("novel-view path helpers are a later row (SURVEY.md §8f-4)")
+        """VR:359-419: spiral camera path around the given poses ([n_frames, 4, 4])."""
+        if n_frames is None:
+            n_frames = getattr(cfg, "render_num", 30)
+        poses = poses.cpu().numpy() if torch.is_tensor(poses) else np.asarray(poses)
+        return spiral_poses(poses, int(n_frames), n_rots, zrate)
 
-    def render_path(self, *a, **kw):
-        raise NotImplementedError("novel-view path helpers are a later row (SURVEY.md §8f-4)")
+    def render_path(self, render_poses, hwf, intrinsics=None, chunk_size=None):
+        """VR:421-509: rgb [N,H,W,3] and disp [N,H,W] of every pose, clipped like the
+        reference (rgb to [0,1], disp to [0, max]). Errors propagate (the reference
+        substitutes black frames)."""
+        H, W, focal = hwf
+        H, W = int(H), int(W)
+        if intrinsics is None:
+            K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
+        else:
+            K = intrinsics.cpu().numpy() if torch.is_tensor(intrinsics) else np.asarray(intrinsics)
+        self._sync_weights()
+        rgbs, disps = [], []
+        for pose in render_poses:
+            pose = pose.cpu().numpy() if torch.is_tensor(pose) else np.asarray(pose, np.float32)
+            with torch.no_grad():
+                res = self.pipeline.render_image(H, W, pose, K)
+            key = "rgb_map" if "rgb_map" in res else "rgb_map_0"
+            rgb = res[key].view(H, W, 3).cpu().numpy()
+            disp = res[key.replace("rgb", "disp")].view(H, W).cpu().numpy()
+            mx = np.max(disp)
+            rgbs.append(np.clip(rgb, 0, 1))
+            disps.append(np.clip(disp, 0, mx if mx > 0 else 1.0))
+        return np.array(rgbs), np.array(disps)
 
     def render_novel_view_sequence(self, *a, **kw):
-        raise NotImplementedError("novel-view path helpers are a later row (SURVEY.md §8f-4)")
+        raise NotImplementedError("writing image/video sequences is outside the render hot path")
 
     def create_video_from_result_images(self, *a, **kw):
         raise NotImplementedError("video encoding is outside the render hot path")

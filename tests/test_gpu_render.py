@@ -342,3 +342,35 @@ def test_renderer_plugin_contract(dev):
     assert out["rgb_map"].device.type == "cuda"
     assert max_err(out["rgb_map_0"].cpu().numpy(), z["out_rgb_map_0"]) < TOL
     reset()
+
+
+def test_renderer_spiral_render_path(dev):
+    """generate_spiral_poses + render_path (VR:359-509) through the plugin: one
+    image per pose, equal to render(batch) of the same pose, clipped like the
+    reference."""
+    from src.config import cfg, reset
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    from nerfhip.synthetic import load_into_network
+    z = load("f1_c2_crop")
+    reset()
+    cfg.task_arg.perturb = 0
+    cfg.enable_ess = False
+    cfg.enable_ert = False
+    net = Network().to(dev)
+    load_into_network(net, params_of(z))
+    net.eval()
+    rend = Renderer(net)
+    poses = rend.generate_spiral_poses(load("lego_test_cameras")["poses"], n_frames=3)
+    H, W = 12, 20
+    focal = 30.0
+    rgbs, disps = rend.render_path(poses, (H, W, focal))
+    assert rgbs.shape == (3, H, W, 3) and disps.shape == (3, H, W)
+    assert rgbs.min() >= 0 and rgbs.max() <= 1
+    K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
+    batch = {"H": H, "W": W, "pose": torch.from_numpy(poses[1].astype(np.float32))[None],
+             "intrinsics": torch.from_numpy(K)[None]}
+    with torch.no_grad():
+        one = rend.render(batch)
+    np.testing.assert_array_equal(rgbs[1], np.clip(one["rgb_map"].cpu().numpy(), 0, 1))
+    reset()
