@@ -116,7 +116,13 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv
     if constexpr ((G & 1) == 0) mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
     else mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], y, bv[Cfg::bsel(G)]);
     __builtin_amdgcn_sched_barrier(0);
-#if MLP_X3_STAGGER
+#if defined(ABL_DMA_BURST)   // timing only: all 4 pieces after group 0
+    if constexpr (G == 0) {
+      if (dma.live) {
+        stage_piece<0>(dma); stage_piece<1>(dma); stage_piece<2>(dma); stage_piece<3>(dma);
+      }
+    }
+#elif MLP_X3_STAGGER
     if constexpr (G / 2 < kBlocksPerWave) {
       if (dma.live && (G & 1) == (dma.wave >> 2)) stage_piece<G / 2>(dma);
     }
@@ -288,9 +294,9 @@ struct EpiHook {
       Op v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-#if defined(ABL_NOEPI)
-        v[r] = acc[2 * G][r];
-        v[4 + r] = acc[2 * G + 1][r];
+#if defined(ABL_NOEPI)   // timing only; still consumes the prefetched biases
+        v[r] = acc[2 * G][r] + bb[G & 1][0][r];
+        v[4 + r] = acc[2 * G + 1][r] + bb[G & 1][1][r];
 #else
         v[r] = fmaxf(__builtin_fmaf(acc[2 * G][r], inv, bb[G & 1][0][r]), floor);
         v[4 + r] = fmaxf(__builtin_fmaf(acc[2 * G + 1][r], inv, bb[G & 1][1][r]), floor);

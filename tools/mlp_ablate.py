@@ -28,7 +28,10 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"],
             "x3_stagger": ["-DMLP_X3_STAGGER=1"], "x3_halflds": ["-DABL_HALFLDS"],
             "x3_halflds_nodma": ["-DABL_HALFLDS", "-DABL_NODMA"],
-            "x3_noepi": ["-DABL_NOEPI"]}
+            "x3_noepi": ["-DABL_NOEPI"],
+            "x3_dmaburst": ["-DABL_DMA_BURST"],
+            "x3_nodma_noepi": ["-DABL_NODMA", "-DABL_NOEPI"],
+            "x3_floor": ["-DABL_NODMA", "-DABL_NOEPI", "-DABL_HALFLDS", "-DABL_NOBAR"]}
 
 
 def is_x3(v):
@@ -38,8 +41,19 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=o
 
 
 def build(names):
+    """Build each variant's library; refuses a variant whose ISA reuses a register
+    with an asm LDS read in flight (tools/check_async_lds.py)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import check_async_lds
     os.makedirs(OUT, exist_ok=True)
     for v in names:
+        src = "mlp_x3.hip" if is_x3(v) else "mlp_fused.hip"
+        asm = os.path.join(OUT, f"{v}.s")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", *[f for f in FLAGS if f != "-shared"],
+                               *VARIANTS[v], "--offload-device-only", "-S",
+                               os.path.join(PKG, "csrc", src), "-o", asm])
+        if check_async_lds.main(asm) != 0:
+            raise SystemExit(f"variant {v}: async LDS-read hazard in its ISA; not built")
         src = "mlp_x3.hip" if is_x3(v) else "mlp_fused.hip"
         cmd = ["/opt/rocm/bin/hipcc", *FLAGS, *VARIANTS[v], os.path.join(PKG, "csrc", "runtime.hip"),
                os.path.join(PKG, "csrc", src), "-o", os.path.join(OUT, f"lib_{v}.so")]
