@@ -26,10 +26,10 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             # the 3-term FP16 split kernel (mlp_x3.hip) and its ablations
             "x3": [], "x3_nodma": ["-DABL_NODMA"], "x3_nobar": ["-DABL_NOBAR"],
             "x3_nobar_nodma": ["-DABL_NOBAR", "-DABL_NODMA"],
-            "x3_stagger": ["-DMLP_X3_STAGGER=1"], "x3_halflds": ["-DABL_HALFLDS"],
+            "x3_stagger": ["-DMLP_X3_SPREAD_DMA", "-DMLP_X3_STAGGER=1"], "x3_halflds": ["-DABL_HALFLDS"],
             "x3_halflds_nodma": ["-DABL_HALFLDS", "-DABL_NODMA"],
             "x3_noepi": ["-DABL_NOEPI"],
-            "x3_dmaburst": ["-DABL_DMA_BURST"],
+            "x3_spread": ["-DMLP_X3_SPREAD_DMA"],
             "x3_nodma_noepi": ["-DABL_NODMA", "-DABL_NOEPI"],
             "x3_floor": ["-DABL_NODMA", "-DABL_NOEPI", "-DABL_HALFLDS", "-DABL_NOBAR"]}
 
