@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kThreads, 2) void mlp_fused_kernel(
 
   // prologue: slices 0, 1, 2 in flight; slice 3 is staged while slice 0 runs
   for (int t = 0; t < 3; ++t)
-    stage_slice(make_dma(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane));
+    stage_slice(make_dma(slices, t, R.buf(t), wave, lane));
   for (int i = tid; i < kHeadFloats / 4; i += kThreads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 

@@ -39,6 +39,44 @@ constexpr int kHeadScales = 3080;     // mlp_x3: per-layer weight scale exponent
 // DMA of one future slice by one wave, spread over the MFMA groups of the
 // current one: this lane's source (block wave*4 of the slice) and the wave's
 // LDS destination; live is false when there is no slice left to stage.
+// MLP_DMA_BUF: the pieces as `buffer_load_dwordx4 ... lds` against one buffer
+// descriptor of the packed network: the slice's byte offset rides in an SGPR
+// (soffset) and each lane's 32-bit offset in the wave's 4 blocks is constant
+// for the whole kernel, instead of a 64-bit per-lane address per slice.
+#ifndef MLP_DMA_BUF
+#define MLP_DMA_BUF 0
+#endif
+
+#if MLP_DMA_BUF
+struct Dma {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned soff;   // slice byte offset (wave-uniform)
+  unsigned voff;   // this lane's byte offset in the slice: block wave*4, lane
+  float* dst;
+  int wave;
+  int live;
+};
+
+// slice t of the packed network at `slices` (t >= kSlices: nothing to stage)
+__device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf, int wave,
+                                        int lane) {
+  const int b = wave * kBlocksPerWave;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)slices, 0, kSlices * kSliceFloats * 4, 0x00020000);
+  return Dma{r, (unsigned)__builtin_amdgcn_readfirstlane(t * kSliceFloats * 4),
+             (unsigned)((b * 64 + lane) * 16), buf + b * 256, wave,
+             __builtin_amdgcn_readfirstlane(t < kSlices ? 1 : 0)};
+}
+
+template <int J>
+__device__ __forceinline__ void stage_piece(const Dma& d) {
+#if defined(ABL_NODMA)
+  return;
+#endif
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_ptr_t)d.dst, 16, d.voff, d.soff,
+                                           J * 1024, 0);
+}
+#else
 struct Dma {
   const float4* src;
   float* dst;
@@ -46,8 +84,11 @@ struct Dma {
   int live;    // wave-uniform: a slice is left to stage
 };
 
-__device__ __forceinline__ Dma make_dma(const float4* slice, float* buf, int wave, int lane) {
+// slice t of the packed network at `slices` (t >= kSlices: nothing to stage)
+__device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf, int wave,
+                                        int lane) {
   const int b = wave * kBlocksPerWave;
+  const float4* slice = t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr;
   return Dma{slice + b * 64 + lane, buf + b * 256, wave,
              __builtin_amdgcn_readfirstlane(slice != nullptr ? 1 : 0)};
 }
@@ -59,6 +100,7 @@ __device__ __forceinline__ void stage_piece(const Dma& d) {
 #endif
   __builtin_amdgcn_global_load_lds((const void*)d.src, (lds_ptr_t)d.dst, 16, J * 1024, 0);
 }
+#endif
 
 // all 4 pieces of a slice (prologue)
 __device__ __forceinline__ void stage_slice(const Dma& d) {
@@ -102,8 +144,7 @@ struct Ring {
   __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
   __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
     const int t = g + 3;
-    return make_dma(t < kSlices ? slices + (size_t)t * (kSliceFloats / 4) : nullptr, buf(t),
-                    wave, lane);
+    return make_dma(slices, t, buf(t), wave, lane);
   }
 };
 

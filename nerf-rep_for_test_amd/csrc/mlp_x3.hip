@@ -44,6 +44,9 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 #ifndef MLP_X3_STAGGER
 #define MLP_X3_STAGGER 0
 #endif
+#ifndef MLP_X3_MIXASM   // operand split as 4 hand-placed v_fma_mix per value pair
+#define MLP_X3_MIXASM 1
+#endif
 
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
@@ -97,18 +100,38 @@ __device__ __forceinline__ void mfma3x2(f32x4& c0, f32x4& c1, const Frags& a, co
   c1 = MFMA16(a.l1, bh, c1);
 }
 
+// Cross-slice fragment prefetch: the last group of a slice issues the reads of
+// the NEXT slice's group 0 (register set x), so a slice starts its MFMAs right
+// after the barrier instead of exposing one LDS latency per slice. The next
+// slice must then be visible one barrier earlier: x3_slice_end certifies slice
+// g+2 at the end of slice g.
+#ifndef MLP_X3_XPF
+#define MLP_X3_XPF 1
+#endif
+
+// The fragment register sets, live across slices (x: even groups, y: odd).
+struct FragPipe {
+  Frags x, y;
+};
+
 // Group G of NG: drain its fragment reads (issued one group earlier), issue
-// group G+1's into the other register set, 6 MFMAs, the wave's LDS-DMA pieces
-// of the slice three ahead (after group 0), then the slice's hook for group G:
+// group G+1's into the other register set (the last group: the next slice's
+// group 0 at LDS base nbase, when NEXT), 6 MFMAs, the wave's LDS-DMA pieces of
+// the slice three ahead (after group 0), then the slice's hook for group G:
 // VALU work that fills the MFMA shadows (epilogue / operand split, below).
-template <int G, int NG, typename Cfg, typename Acc, typename BV, typename Hook>
-__device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv, Frags& x,
-                                           Frags& y, const Dma& dma, Hook& hook) {
+template <int G, int NG, typename Cfg, bool NEXT, typename Acc, typename BV, typename Hook>
+__device__ __forceinline__ void run_group3(Acc& acc, unsigned base, unsigned nbase, const BV& bv,
+                                           FragPipe& fp, const Dma& dma, Hook& hook) {
+  Frags& x = fp.x;
+  Frags& y = fp.y;
   if constexpr (G < NG) {
     lds_drain();
     if constexpr (G + 1 < NG) {
       if constexpr ((G & 1) == 0) load_frags<G + 1>(y, base);
       else load_frags<G + 1>(x, base);
+    } else if constexpr (NEXT && MLP_X3_XPF) {
+      static_assert((G & 1) == 1, "the last group computes from set y");
+      load_frags<0>(x, nbase);
     }
     hook.template prefetch<G>();   // the hook's own LDS reads, drained with the frags
     __builtin_amdgcn_sched_barrier(0);
@@ -135,18 +158,34 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, const BV& bv
 #endif
     hook.template after<G>(acc);
     __builtin_amdgcn_sched_barrier(0);
-    run_group3<G + 1, NG, Cfg>(acc, base, bv, x, y, dma, hook);
+    run_group3<G + 1, NG, Cfg, NEXT>(acc, base, nbase, bv, fp, dma, hook);
   }
 }
 
-template <int NG, typename Cfg, typename Acc, typename BV, typename Hook>
-__device__ __forceinline__ void run_slice3(Acc& acc, const float* buf, int lane, const BV& bv,
-                                           const Dma& dma, Hook& hook) {
-  const unsigned base = lds_base(buf, lane);
-  Frags x, y;
-  load_frags<0>(x, base);
-  y = x;
-  run_group3<0, NG, Cfg>(acc, base, bv, x, y, dma, hook);
+// Slice g of the stream (NG groups). With MLP_X3_XPF its group 0 fragments were
+// issued by the previous slice's last group (or the kernel prologue).
+template <int NG, typename Cfg, bool NEXT = true, typename Acc, typename BV, typename Hook>
+__device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const BV& bv,
+                                           FragPipe& fp, Hook& hook) {
+  const unsigned base = lds_base(R.buf(g), R.lane);
+#if !MLP_X3_XPF
+  load_frags<0>(fp.x, base);
+#endif
+  run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp, R.dma_for(g),
+                               hook);
+}
+
+// End of slice g: this wave's LDS-DMA of slice g+2 (XPF; g+1 without) has
+// landed, then one barrier publishes it to every wave and frees slice g's
+// buffer for the DMA issued in slice g+1. INFLIGHT = slices of DMA allowed in
+// flight without the prefetch (2 while the stream has three slices ahead).
+template <int INFLIGHT>
+__device__ __forceinline__ void x3_slice_end() {
+#if MLP_X3_XPF
+  slice_end<(INFLIGHT > 0 ? INFLIGHT - 1 : 0)>();
+#else
+  slice_end<INFLIGHT>();
+#endif
 }
 
 // Slice shapes: the tiles, the B operand and whether the group starts its
@@ -190,6 +229,19 @@ __device__ __forceinline__ void split2(float a, float b, float s, float& hp, flo
   hp = __builtin_bit_cast(float, half2_t{(_Float16)a, (_Float16)b});
   lp = hp;
   (void)s;
+#elif MLP_X3_MIXASM
+  // hi = f16(a*s), lo = f16(a*s - hi): one mixed-precision fma each (a*s is
+  // exact: s is a power of two), written straight into the halves of the packed
+  // registers; the residual reads hi's f16 half in place (op_sel). 4 VALU per
+  // pair (hipcc's form: 7, with a second, FP32 route to the packed hi pair).
+  float h, l;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(a), "v"(s));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(b), "v"(s));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(a), "v"(s), "v"(h));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(l) : "v"(b), "v"(s), "v"(h));
+  hp = h;
+  lp = l;
 #else
   // hi = f16(a*s), lo = f16(a*s - hi): one mixed-precision fma each (a*s is
   // exact: s is a power of two)
@@ -365,14 +417,14 @@ __device__ __forceinline__ float op_absmax(const Op& v) {
 // One 256-row slice (K step Q of operand array B) + its end-of-slice sync.
 template <int Q, bool FIRST, typename BV, typename Hook>
 __device__ __forceinline__ void slice256x(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
-                                          Hook& hook) {
-  run_slice3<8, Step256<Q, FIRST>>(acc, R.buf(g), R.lane, b, R.dma_for(g), hook);
-  slice_end<2>();
+                                          FragPipe& fp, Hook& hook) {
+  run_slice3<8, Step256<Q, FIRST>>(acc, R, g, b, fp, hook);
+  x3_slice_end<2>();
 }
 template <int Q, typename BV, typename Hook>
 __device__ __forceinline__ void slice256(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
-                                         Hook& hook) {
-  slice256x<Q, false>(acc, R, g, b, hook);
+                                         FragPipe& fp, Hook& hook) {
+  slice256x<Q, false>(acc, R, g, b, fp, hook);
 }
 
 // A whole epilogue outside a slice (skip layer): each pair's biases, then it.
@@ -391,15 +443,15 @@ __device__ __forceinline__ void epi_pairs(EpiHook& epi, f32x4 (&acc)[16]) {
 // last runs the fused epilogue (disabled for the skip layer, whose two
 // encoding slices follow).
 __device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int g, Op (&X)[8],
-                                           float s, EpiHook& epi) {
-  { SplitHook h{X[1], s}; slice256x<0, true>(acc, R, g + 0, X, h); }
-  { SplitHook h{X[2], s}; slice256<1>(acc, R, g + 1, X, h); }
-  { SplitHook h{X[3], s}; slice256<2>(acc, R, g + 2, X, h); }
-  { SplitHook h{X[4], s}; slice256<3>(acc, R, g + 3, X, h); }
-  { SplitHook h{X[5], s}; slice256<4>(acc, R, g + 4, X, h); }
-  { SplitHook h{X[6], s}; slice256<5>(acc, R, g + 5, X, h); }
-  { SplitHook h{X[7], s}; slice256<6>(acc, R, g + 6, X, h); }
-  slice256<7>(acc, R, g + 7, X, epi);
+                                           float s, FragPipe& fp, EpiHook& epi) {
+  { SplitHook h{X[1], s}; slice256x<0, true>(acc, R, g + 0, X, fp, h); }
+  { SplitHook h{X[2], s}; slice256<1>(acc, R, g + 1, X, fp, h); }
+  { SplitHook h{X[3], s}; slice256<2>(acc, R, g + 2, X, fp, h); }
+  { SplitHook h{X[4], s}; slice256<3>(acc, R, g + 3, X, fp, h); }
+  { SplitHook h{X[5], s}; slice256<4>(acc, R, g + 4, X, fp, h); }
+  { SplitHook h{X[6], s}; slice256<5>(acc, R, g + 5, X, fp, h); }
+  { SplitHook h{X[7], s}; slice256<6>(acc, R, g + 6, X, fp, h); }
+  slice256<7>(acc, R, g + 7, X, fp, epi);
   epi.finish(acc);
 }
 
@@ -418,7 +470,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const Ring R{ring, slices, wave, lane};
 
   for (int t = 0; t < 3; ++t)
-    stage_slice(make_dma(slices + (size_t)t * (kSliceFloats / 4), R.buf(t), wave, lane));
+    stage_slice(make_dma(slices, t, R.buf(t), wave, lane));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
@@ -440,7 +492,11 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 
   f32x4 acc[16];   // every layer's first slice starts it from zero
   Op X[8];
+  FragPipe fp;
   __syncthreads();   // head, z/rays loads and the three prologue slices resident
+#if MLP_X3_XPF
+  load_frags<0>(fp.x, lds_base(R.buf(0), lane));   // slice 0, group 0
+#endif
 
   // ---- layer 0: 63 -> 256 (slices 0, 1), epilogue fused into slice 1 --------
   int e = act_exponent(enc_max);
@@ -450,10 +506,10 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     split_op(E[0], s);
     split_op(E[1], s);
     NoHook nh;
-    slice256x<0, true>(acc, R, 0, E, nh);
+    slice256x<0, true>(acc, R, 0, E, fp, nh);
     EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 0] + e)), 0.0f,
                 lds_addr(hd + kHeadBias + g4 * 64), nullptr, 0.0f, 0.0f, true};
-    slice256<1>(acc, R, 1, E, epi);
+    slice256<1>(acc, R, 1, E, fp, epi);
     epi.finish(acc);
     e = act_exponent(sample_max(epi.amax));
   }
@@ -467,12 +523,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)),
                 L != 8 ? 0.0f : -__builtin_inff(), lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
                 L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
-    act_slices(acc, R, g, X, s, epi);
+    act_slices(acc, R, g, X, s, fp, epi);
     g += 8;
     if (L == 5) {   // cat(input_pts, h) (NET:57-58): the encoding's K steps last
       NoHook nh;
-      slice256<0>(acc, R, g, encf, nh);
-      slice256<1>(acc, R, g + 1, encf, nh);
+      slice256<0>(acc, R, g, encf, fp, nh);
+      slice256<1>(acc, R, g + 1, encf, fp, nh);
       g += 2;
       epi.on = true;   // this layer's epilogue, not pipelined
       epi_pairs<0>(epi, acc);
@@ -508,16 +564,16 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   {
     // views slice k reads operands 2k, 2k+1 and splits 2k+2, 2k+3 (then dir)
     Split2 h0{{X[2], s}, {X[3], s}};
-    run_slice3<8, StepViews<0, true>>(acc8, R.buf(g), lane, X, R.dma_for(g), h0); slice_end<2>();
+    run_slice3<8, StepViews<0, true>>(acc8, R, g, X, fp, h0); x3_slice_end<2>();
     Split2 h1{{X[4], s}, {X[5], s}};
-    run_slice3<8, StepViews<2>>(acc8, R.buf(g + 1), lane, X, R.dma_for(g + 1), h1); slice_end<2>();
+    run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>();
     Split2 h2{{X[6], s}, {X[7], s}};
-    run_slice3<8, StepViews<4>>(acc8, R.buf(g + 2), lane, X, R.dma_for(g + 2), h2); slice_end<1>();
+    run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<1>();
     SplitHook h3{dirf, s};
-    run_slice3<8, StepViews<6>>(acc8, R.buf(g + 3), lane, X, R.dma_for(g + 3), h3); slice_end<0>();
+    run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<0>();
     NoHook nh;
     const Op D[1] = {dirf};
-    run_slice3<4, Step256<0>>(acc8, R.buf(g + 4), lane, D, R.dma_for(g + 4), nh);
+    run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh);   // the stream's last slice
   }
   {   // views epilogue (bias, ReLU) -- once per pass, not pipelined
     const float inv = ldexpf(1.0f, -((int)hd[kHeadScales + 9] + e));

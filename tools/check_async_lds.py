@@ -22,8 +22,46 @@ def regs(tok):
     return set()
 
 
+def _parse(t):
+    op = t.split()[0]
+    ops = [x.strip() for x in t[len(op):].split(",")]
+    used = set()
+    for o in ops:
+        used |= regs(o.split()[0] if o else "")
+    return op, ops, used
+
+
+def _scan_edge(lines, start, pending, path, src):
+    """Reads still pending at a backward branch (src) flow to its target: check the
+    target's instructions up to the first lgkmcnt(0) drain."""
+    bad = 0
+    for j in range(start, len(lines)):
+        t = lines[j].strip()
+        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
+            continue
+        op, ops, used = _parse(t)
+        if op == "s_waitcnt" and "lgkmcnt(0)" in t:
+            break
+        if op == "ds_read_b128":
+            hit = regs(ops[0]) & set(pending)
+        elif op.startswith("s_") and not op.startswith("s_waitcnt"):
+            continue
+        else:
+            hit = used & set(pending)
+        if hit:
+            print(f"{path}:{j + 1}: '{t}' touches regs {sorted(hit)} still pending at the "
+                  f"loop branch on line {src + 1}")
+            bad += 1
+    return bad
+
+
 def main(path):
     lines = open(path).read().split("\n")
+    labels = {}
+    for i, raw in enumerate(lines):
+        m = re.match(r"^(\.?[A-Za-z_$][\w.$]*):", raw.strip())
+        if m:
+            labels[m.group(1)] = i
     pending = {}   # reg -> line of the asm read
     in_asm = False
     bad = 0
@@ -53,6 +91,11 @@ def main(path):
                 bad += 1
             for r in dst:
                 pending[r] = i + 1
+            continue
+        if (op.startswith("s_cbranch") or op == "s_branch") and pending:
+            tgt = labels.get(ops[0])
+            if tgt is not None and tgt < i:   # loop back edge
+                bad += _scan_edge(lines, tgt, pending, path, i)
             continue
         if op.startswith("s_") and not op.startswith("s_waitcnt"):
             continue

@@ -31,7 +31,13 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_noepi": ["-DABL_NOEPI"],
             "x3_spread": ["-DMLP_X3_SPREAD_DMA"],
             "x3_nodma_noepi": ["-DABL_NODMA", "-DABL_NOEPI"],
-            "x3_floor": ["-DABL_NODMA", "-DABL_NOEPI", "-DABL_HALFLDS", "-DABL_NOBAR"]}
+            "x3_floor": ["-DABL_NODMA", "-DABL_NOEPI", "-DABL_HALFLDS", "-DABL_NOBAR"],
+            # cross-slice fragment prefetch off (the previous schedule)
+            "x3_noxpf": ["-DMLP_X3_XPF=0"],
+            # weight DMA as buffer_load ... lds (SGPR slice offset, constant lane offset)
+            "x3_buf": ["-DMLP_DMA_BUF=1"],
+            # operand split in hipcc's 7-instruction form
+            "x3_nomix": ["-DMLP_X3_MIXASM=0"]}
 
 
 def is_x3(v):
@@ -100,11 +106,21 @@ def run(names, rounds, n_rays, S):
             if r > 0:
                 times[v].append(e0.elapsed_time(e1))
     flops = n_rays * S * 1186816
+    ref = None
     for v in names:
         t = sorted(times[v])
         med = t[len(t) // 2]
+        sl, hd = packed[is_x3(v)]
+        raw.zero_()
+        libs[v](sl.data_ptr(), hd.data_ptr(), ro.data_ptr(), rd.data_ptr(), z.data_ptr(), 0,
+                n_rays, S, raw.data_ptr(), stream)
+        torch.cuda.synchronize()
+        out = raw.clone()
+        if ref is None:
+            ref = out
+        diff = float((out - ref).abs().max())
         print(f"{v:14s} median {med:8.2f} ms  min {t[0]:8.2f}  TF {flops / med / 1e9:7.1f}  "
-              f"frac {flops / med / 1e9 / 157.3:.3f}", flush=True)
+              f"frac {flops / med / 1e9 / 157.3:.3f}  maxdiff_vs_{names[0]} {diff:.3g}", flush=True)
 
 
 if __name__ == "__main__":
