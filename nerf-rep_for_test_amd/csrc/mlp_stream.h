@@ -57,24 +57,32 @@ struct Dma {
   int live;
 };
 
-// slice t of the packed network at `slices` (t >= kSlices: nothing to stage)
-__device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf, int wave,
-                                        int lane) {
-  const int b = wave * kBlocksPerWave;
+// blocks b0.. of slice t of the packed network at `slices` (t >= kSlices or
+// !live: nothing to stage)
+__device__ __forceinline__ Dma make_dma_blocks(const float4* slices, int t, float* buf, int b0,
+                                               int wave, int lane, bool live) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)slices, 0, kSlices * kSliceFloats * 4, 0x00020000);
   return Dma{r, (unsigned)__builtin_amdgcn_readfirstlane(t * kSliceFloats * 4),
-             (unsigned)((b * 64 + lane) * 16), buf + b * 256, wave,
-             __builtin_amdgcn_readfirstlane(t < kSlices ? 1 : 0)};
+             (unsigned)((b0 * 64 + lane) * 16), buf + b0 * 256, wave,
+             __builtin_amdgcn_readfirstlane(live && t < kSlices ? 1 : 0)};
 }
 
+// slice t of the packed network at `slices` (t >= kSlices: nothing to stage)
+__device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf, int wave,
+                                        int lane) {
+  return make_dma_blocks(slices, t, buf, wave * kBlocksPerWave, wave, lane, true);
+}
+
+// piece J (0..7) of the wave's blocks: the 12-bit instruction offset reaches
+// pieces 0-3; pieces 4-7 move the LDS base and soffset by 4 KiB
 template <int J>
 __device__ __forceinline__ void stage_piece(const Dma& d) {
 #if defined(ABL_NODMA)
   return;
 #endif
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_ptr_t)d.dst, 16, d.voff, d.soff,
-                                           J * 1024, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_ptr_t)(d.dst + (J / 4) * 1024), 16,
+                                           d.voff, d.soff + (J / 4) * 4096, (J % 4) * 1024, 0);
 }
 #else
 struct Dma {
@@ -148,15 +156,13 @@ struct Ring {
   }
 };
 
-template <int PENDING>   // slices (of 4 pieces) allowed to stay in flight
+// PENDING slices (of PIECES pieces each per wave) allowed to stay in flight
+template <int PENDING, int PIECES = 4>
 __device__ __forceinline__ void slice_end() {
 #if !defined(ABL_NOBAR)
-  if constexpr (PENDING >= 2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (PENDING == 1)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  constexpr int n = (PENDING >= 2 ? 2 : PENDING) * PIECES;
+  static_assert(n < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(n) : "memory");
   __builtin_amdgcn_s_barrier();
 #endif
   __builtin_amdgcn_sched_barrier(0);

@@ -25,6 +25,11 @@
 // and rows 16m + 4(l>>4) + r. K step q of the next layer takes, on lane group
 // g = l>>4, slots j = 0..7 = rows 16(2q + (j>>2)) + 4g + (j&3), i.e. registers
 // r of tiles 2q and 2q+1 (nerfhip/pack.py packs W with that K permutation).
+// this kernel's weight stream: buffer-form LDS-DMA (mlp_stream.h), issued by
+// waves 0-3 only (MLP_X3_LOADERS below)
+#ifndef MLP_DMA_BUF
+#define MLP_DMA_BUF 1
+#endif
 #include "mlp_stream.h"
 
 namespace nerfhip {
@@ -43,6 +48,9 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 
 #ifndef MLP_X3_STAGGER
 #define MLP_X3_STAGGER 0
+#endif
+#ifndef MLP_X3_ILV   // >0: interleave the hook's VALU into the group's MFMAs (per gap)
+#define MLP_X3_ILV 2
 #endif
 #ifndef MLP_X3_MIXASM   // operand split as 4 hand-placed v_fma_mix per value pair
 #define MLP_X3_MIXASM 1
@@ -112,7 +120,43 @@ __device__ __forceinline__ void mfma3x2(f32x4& c0, f32x4& c1, const Frags& a, co
 // The fragment register sets, live across slices (x: even groups, y: odd).
 struct FragPipe {
   Frags x, y;
+  int late;   // wave-uniform: this wave runs half a slice behind (MLP_X3_HALF)
 };
+
+// Half-slice stagger (MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7
+// (the SIMD partners of waves 0-3) pass each slice's barrier after its group 3
+// instead of after group 7, so partners run half a slice apart and their VALU
+// bursts (epilogue, splits) land beside the other's MFMAs. Needs the weight
+// DMA two slices ahead (a late wave still reads slice g-1 after barrier g-1)
+// and every barrier to certify the wave's own pieces (vmcnt(0)).
+#ifndef MLP_X3_HALF
+#define MLP_X3_HALF 0
+#endif
+constexpr int kX3DmaAhead = MLP_X3_HALF ? 2 : 3;
+
+// MLP_X3_LOADERS=4: only waves 0-3 stage weights (8 pieces each, buffer form),
+// so a loading wave's SIMD partner keeps issuing MFMAs meanwhile.
+#ifndef MLP_X3_LOADERS
+#define MLP_X3_LOADERS 4
+#endif
+#ifndef MLP_X3_LOADER_SPLIT
+#define MLP_X3_LOADER_SPLIT 0
+#endif
+constexpr int kX3Pieces = MLP_X3_LOADERS == 4 ? 8 : 4;   // per loading wave and slice
+__device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane) {
+#if MLP_X3_LOADERS == 4
+  static_assert(MLP_DMA_BUF, "4 loader waves need the buffer-form DMA");
+  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4);
+#else
+  return make_dma(slices, t, buf, wave, lane);
+#endif
+}
+
+__device__ __forceinline__ void x3_barrier_now() {
+#if MLP_X3_HALF
+  slice_end<0>();
+#endif
+}
 
 // Group G of NG: drain its fragment reads (issued one group earlier), issue
 // group G+1's into the other register set (the last group: the next slice's
@@ -138,8 +182,34 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, unsigned nba
     constexpr int m = Cfg::tile(G);
     if constexpr ((G & 1) == 0) mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
     else mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], y, bv[Cfg::bsel(G)]);
+#if MLP_X3_ILV
+    // the hook's VALU in the gaps of this group's own MFMAs: MFMA, k VALU, ...
+    hook.template after<G>(acc);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, MLP_X3_ILV, 0); // up to k VALU
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
-#if !defined(MLP_X3_SPREAD_DMA)
+#if MLP_X3_LOADERS == 4
+    // waves 0-3 stage 8 pieces each, their partners none
+    if constexpr (G == 0) {
+      if (dma.live) {
+        stage_piece<0>(dma); stage_piece<1>(dma); stage_piece<2>(dma); stage_piece<3>(dma);
+#if !MLP_X3_LOADER_SPLIT
+        stage_piece<4>(dma); stage_piece<5>(dma); stage_piece<6>(dma); stage_piece<7>(dma);
+#endif
+      }
+    }
+#if MLP_X3_LOADER_SPLIT
+    if constexpr (G == MLP_X3_LOADER_SPLIT) {
+      if (dma.live) {
+        stage_piece<4>(dma); stage_piece<5>(dma); stage_piece<6>(dma); stage_piece<7>(dma);
+      }
+    }
+#endif
+#elif !defined(MLP_X3_SPREAD_DMA)
     // the wave's 4 pieces back to back after group 0 (one address/M0 setup;
     // measured +2.4 % over one piece every other group)
     if constexpr (G == 0) {
@@ -156,8 +226,13 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, unsigned nba
       if (dma.live) stage_piece<G / 2>(dma);
     }
 #endif
+#if !MLP_X3_ILV
     hook.template after<G>(acc);
+#endif
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (MLP_X3_HALF && G == 3 && NG == 8) {
+      if (fp.late) x3_barrier_now();
+    }
     run_group3<G + 1, NG, Cfg, NEXT>(acc, base, nbase, bv, fp, dma, hook);
   }
 }
@@ -171,8 +246,9 @@ __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const
 #if !MLP_X3_XPF
   load_frags<0>(fp.x, base);
 #endif
-  run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp, R.dma_for(g),
-                               hook);
+  const int t = g + kX3DmaAhead;
+  run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp,
+                               x3_dma(R.slices, t, R.buf(t), R.wave, R.lane), hook);
 }
 
 // End of slice g: this wave's LDS-DMA of slice g+2 (XPF; g+1 without) has
@@ -180,11 +256,13 @@ __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const
 // buffer for the DMA issued in slice g+1. INFLIGHT = slices of DMA allowed in
 // flight without the prefetch (2 while the stream has three slices ahead).
 template <int INFLIGHT>
-__device__ __forceinline__ void x3_slice_end() {
-#if MLP_X3_XPF
-  slice_end<(INFLIGHT > 0 ? INFLIGHT - 1 : 0)>();
+__device__ __forceinline__ void x3_slice_end(const FragPipe& fp) {
+#if MLP_X3_HALF
+  if (!fp.late) x3_barrier_now();
+#elif MLP_X3_XPF
+  slice_end<(INFLIGHT > 0 ? INFLIGHT - 1 : 0), kX3Pieces>();
 #else
-  slice_end<INFLIGHT>();
+  slice_end<INFLIGHT, kX3Pieces>();
 #endif
 }
 
@@ -419,7 +497,7 @@ template <int Q, bool FIRST, typename BV, typename Hook>
 __device__ __forceinline__ void slice256x(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
                                           FragPipe& fp, Hook& hook) {
   run_slice3<8, Step256<Q, FIRST>>(acc, R, g, b, fp, hook);
-  x3_slice_end<2>();
+  x3_slice_end<2>(fp);
 }
 template <int Q, typename BV, typename Hook>
 __device__ __forceinline__ void slice256(f32x4 (&acc)[16], const Ring& R, int g, const BV& b,
@@ -469,8 +547,8 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const int g4 = lane >> 4;
   const Ring R{ring, slices, wave, lane};
 
-  for (int t = 0; t < 3; ++t)
-    stage_slice(make_dma(slices, t, R.buf(t), wave, lane));
+  for (int t = 0; t < kX3DmaAhead; ++t)
+    stage_slice(make_dma(slices, t, R.buf(t), wave, lane));   // all 8 waves, 4 pieces each
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
@@ -493,6 +571,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   f32x4 acc[16];   // every layer's first slice starts it from zero
   Op X[8];
   FragPipe fp;
+  fp.late = MLP_X3_HALF ? __builtin_amdgcn_readfirstlane(wave >> 2) : 0;
   __syncthreads();   // head, z/rays loads and the three prologue slices resident
 #if MLP_X3_XPF
   load_frags<0>(fp.x, lds_base(R.buf(0), lane));   // slice 0, group 0
@@ -564,13 +643,13 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   {
     // views slice k reads operands 2k, 2k+1 and splits 2k+2, 2k+3 (then dir)
     Split2 h0{{X[2], s}, {X[3], s}};
-    run_slice3<8, StepViews<0, true>>(acc8, R, g, X, fp, h0); x3_slice_end<2>();
+    run_slice3<8, StepViews<0, true>>(acc8, R, g, X, fp, h0); x3_slice_end<2>(fp);
     Split2 h1{{X[4], s}, {X[5], s}};
-    run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>();
+    run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>(fp);
     Split2 h2{{X[6], s}, {X[7], s}};
-    run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<1>();
+    run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<1>(fp);
     SplitHook h3{dirf, s};
-    run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<0>();
+    run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<0>(fp);
     NoHook nh;
     const Op D[1] = {dirf};
     run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh);   // the stream's last slice

@@ -6,6 +6,11 @@ registers are written when the asm issues. This script flags any instruction
 between such a read and its drain that reads or writes one of the pending
 destination VGPRs (a stale read, or a register the late data would clobber).
 
+The pending set is propagated over the control-flow graph of the .s (basic
+blocks split at labels and branches; successors from s_branch / s_cbranch_* /
+fall-through), so reads left in flight across a loop back edge or a branch
+are followed to every instruction they can reach.
+
     python tools/check_async_lds.py build/asm/mlp_x3.s
 """
 import re
@@ -22,49 +27,13 @@ def regs(tok):
     return set()
 
 
-def _parse(t):
-    op = t.split()[0]
-    ops = [x.strip() for x in t[len(op):].split(",")]
-    used = set()
-    for o in ops:
-        used |= regs(o.split()[0] if o else "")
-    return op, ops, used
+LABEL = re.compile(r"^(\.?[A-Za-z_$][\w.$]*):")
 
 
-def _scan_edge(lines, start, pending, path, src):
-    """Reads still pending at a backward branch (src) flow to its target: check the
-    target's instructions up to the first lgkmcnt(0) drain."""
-    bad = 0
-    for j in range(start, len(lines)):
-        t = lines[j].strip()
-        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
-            continue
-        op, ops, used = _parse(t)
-        if op == "s_waitcnt" and "lgkmcnt(0)" in t:
-            break
-        if op == "ds_read_b128":
-            hit = regs(ops[0]) & set(pending)
-        elif op.startswith("s_") and not op.startswith("s_waitcnt"):
-            continue
-        else:
-            hit = used & set(pending)
-        if hit:
-            print(f"{path}:{j + 1}: '{t}' touches regs {sorted(hit)} still pending at the "
-                  f"loop branch on line {src + 1}")
-            bad += 1
-    return bad
-
-
-def main(path):
-    lines = open(path).read().split("\n")
-    labels = {}
-    for i, raw in enumerate(lines):
-        m = re.match(r"^(\.?[A-Za-z_$][\w.$]*):", raw.strip())
-        if m:
-            labels[m.group(1)] = i
-    pending = {}   # reg -> line of the asm read
+def _instructions(lines):
+    """[(line index, text, in_asm)] of the instructions, and labels -> position."""
+    out, labels = [], {}
     in_asm = False
-    bad = 0
     for i, raw in enumerate(lines):
         t = raw.strip()
         if t.startswith(";;#ASMSTART"):
@@ -73,7 +42,52 @@ def main(path):
         if t.startswith(";;#ASMEND"):
             in_asm = False
             continue
-        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
+        m = LABEL.match(t)
+        if m:
+            labels[m.group(1)] = len(out)
+            out.append((i, None, False))        # label marker
+            continue
+        if not t or t.startswith(";") or t.startswith("."):
+            continue
+        out.append((i, t.split(";")[0].strip(), in_asm))
+    return out, labels
+
+
+def _blocks(ins, labels):
+    """Basic blocks as (start, end) positions into ins, and successor lists."""
+    starts = {0}
+    for p, (_, t, _) in enumerate(ins):
+        if t is None:
+            starts.add(p)
+        elif t.startswith("s_branch") or t.startswith("s_cbranch") or t.startswith("s_endpgm") \
+                or t.startswith("s_setpc"):
+            starts.add(p + 1)
+    starts = sorted(s for s in starts if s < len(ins))
+    bounds = list(zip(starts, starts[1:] + [len(ins)]))
+    at = {s: k for k, (s, _) in enumerate(bounds)}
+    succ = []
+    for k, (s, e) in enumerate(bounds):
+        last = next((ins[p][1] for p in range(e - 1, s - 1, -1) if ins[p][1] is not None), "")
+        op = last.split()[0] if last else ""
+        nxt = [k + 1] if k + 1 < len(bounds) else []
+        if op == "s_branch":
+            tgt = labels.get(last.split()[1])
+            succ.append([at[tgt]] if tgt in at else [])
+        elif op.startswith("s_cbranch"):
+            tgt = labels.get(last.split()[1])
+            succ.append(nxt + ([at[tgt]] if tgt in at else []))
+        elif op in ("s_endpgm", "s_setpc_b64"):
+            succ.append([])
+        else:
+            succ.append(nxt)
+    return bounds, succ
+
+
+def _run_block(ins, s, e, pending, report):
+    pending = dict(pending)
+    for p in range(s, e):
+        line, t, in_asm = ins[p]
+        if t is None:
             continue
         op = t.split()[0]
         if op == "s_waitcnt" and "lgkmcnt(0)" in t:
@@ -87,25 +101,51 @@ def main(path):
             dst = regs(ops[0])
             clash = dst & set(pending)
             if clash:
-                print(f"{path}:{i + 1}: asm read overwrites pending regs {sorted(clash)}")
-                bad += 1
+                report(line, f"asm read overwrites pending regs {sorted(clash)}")
             for r in dst:
-                pending[r] = i + 1
-            continue
-        if (op.startswith("s_cbranch") or op == "s_branch") and pending:
-            tgt = labels.get(ops[0])
-            if tgt is not None and tgt < i:   # loop back edge
-                bad += _scan_edge(lines, tgt, pending, path, i)
+                pending[r] = line + 1
             continue
         if op.startswith("s_") and not op.startswith("s_waitcnt"):
             continue
         hit = used & set(pending)
         if hit:
-            print(f"{path}:{i + 1}: '{t}' touches pending LDS-read regs {sorted(hit)} "
-                  f"(read issued at line {pending[min(hit)]})")
-            bad += 1
-    print("violations:", bad)
-    return 1 if bad else 0
+            report(line, f"'{t}' touches pending LDS-read regs {sorted(hit)} "
+                         f"(read issued at line {pending[min(hit)]})")
+    return pending
+
+
+def main(path):
+    lines = open(path).read().split("\n")
+    ins, labels = _instructions(lines)
+    bounds, succ = _blocks(ins, labels)
+    entry = [dict() for _ in bounds]
+    seen = [False] * len(bounds)
+    seen[0] = True
+    work = [0]
+    while work:                                 # forward dataflow to a fixpoint
+        k = work.pop()
+        out = _run_block(ins, *bounds[k], entry[k], lambda *a: None)
+        for n in succ[k]:
+            merged = dict(entry[n])
+            changed = not seen[n]
+            for r, v in out.items():
+                if r not in merged:
+                    merged[r] = v
+                    changed = True
+            if changed:
+                entry[n], seen[n] = merged, True
+                work.append(n)
+    found = {}
+
+    def report(line, msg):
+        found.setdefault(line, msg)
+    for k in range(len(bounds)):
+        if seen[k]:
+            _run_block(ins, *bounds[k], entry[k], report)
+    for line in sorted(found):
+        print(f"{path}:{line + 1}: {found[line]}")
+    print("violations:", len(found))
+    return 1 if found else 0
 
 
 if __name__ == "__main__":

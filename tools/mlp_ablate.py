@@ -37,7 +37,17 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             # weight DMA as buffer_load ... lds (SGPR slice offset, constant lane offset)
             "x3_buf": ["-DMLP_DMA_BUF=1"],
             # operand split in hipcc's 7-instruction form
-            "x3_nomix": ["-DMLP_X3_MIXASM=0"]}
+            "x3_nomix": ["-DMLP_X3_MIXASM=0"],
+            # waves 4-7 half a slice behind (DMA two slices ahead)
+            "x3_half": ["-DMLP_X3_HALF=1"],
+            # weight DMA from waves 0-3 only (8 pieces each), back to back / split 4+4
+            "x3_ld4": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4"],
+            "x3_ld4s": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_LOADER_SPLIT=2"],
+            # the previous defaults: all 8 waves load (global form), hook VALU after the MFMAs
+            "x3_prev": ["-DMLP_DMA_BUF=0", "-DMLP_X3_LOADERS=8", "-DMLP_X3_ILV=0"],
+            # hook VALU interleaved into the group's MFMAs, 2 / 4 per gap
+            "x3_ilv2": ["-DMLP_X3_ILV=2"], "x3_ilv4": ["-DMLP_X3_ILV=4"],
+            "x3_ld4_ilv2": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_ILV=2"]}
 
 
 def is_x3(v):
