@@ -82,6 +82,29 @@ int nerf_mlp_forward_x3(const float* w_slices, const float* w_head,
                         const float* z, int64_t z_stride, int64_t n, int S,
                         float* raw, nerf_stream_t stream);
 
+/* Training MLP (BASELINE configs[2]): the 8x256 NeRF MLP of a training step
+ * (network.py:49-74 forward and its autograd backward) as layer GEMMs over
+ * feature-major activations ([F][P]: row f = feature f of every sample),
+ * FP32 operands as 3-term FP16 splits on FP16 MFMA (see nerf_mlp_forward_x3).
+ *
+ * nerf_x3_layer: C[m][p] = 2^-(w_scale+e_p) * sum_k W[m][k] B[k][p]
+ *   (+ bias[m]) (+ ru[m] * rw[p]) (ReLU if relu) (* (mask[m][p] > 0)),
+ *   m < 16*m_tiles, k < 32*k_steps; W packed by nerfhip.train_mlp.pack_x3_matrix
+ *   with its scale exponent in *w_scale (device int). The (shape, epilogue)
+ *   instances are those the training MLP launches (nerf-rep_for_test_amd/csrc/
+ *   mlp_x3.hip); others return NERF_E_UNSUPPORTED. amax_out (optional, device
+ *   float, caller-initialised) is raised to max |C|.
+ * nerf_x3_wgrad: part[c][m][n] = sum over samples p in [c*chunk, (c+1)*chunk)
+ *   of A[m][p] * B[n][p]; amax_a / amax_b = device max|A|, max|B|; bias_part
+ *   (optional) [c][m] = sum over the chunk's samples of A[m][p]. */
+int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
+                  const float* bias, const float* B, int64_t ldb, const float* mask,
+                  int64_t ldm, const float* ru, const float* rw, int relu, float* C,
+                  int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream);
+int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
+                  int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
+                  float* part, float* bias_part, nerf_stream_t stream);
+
 /* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
  * Reductions follow torch's CPU float32 summation order.
  * Outputs rgb[n][3], disp/acc/depth[n]; weights[n][S] optional (NULL). */

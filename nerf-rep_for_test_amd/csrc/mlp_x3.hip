@@ -460,7 +460,11 @@ __device__ __forceinline__ void encode_xyz(const float (&p)[3], int g, Op (&e)[2
       const int f = pr / 3, c = pr - 3 * f;
       const float x = c == 0 ? p[0] : (c == 1 ? p[1] : p[2]);
       const float arg = x * (float)(1 << f);   // exact power of two (freq.py:19)
+#if defined(ABL_NOENC)   // timing only
+      a = arg; b = arg * 0.5f;
+#else
       sincosf(arg, &a, &b);
+#endif
     } else {
       a = t == 6 ? p[0] : (t == 7 ? p[2] : 0.0f);
       b = t == 6 ? p[1] : 0.0f;
@@ -477,7 +481,11 @@ __device__ __forceinline__ void encode_dir(const float (&d)[3], int g, Op& e) {
   for (int t = 0; t < 3; ++t) {
     const float arg = d[t] * (float)(1 << g);
     float sv, cv;
+#if defined(ABL_NOENC)   // timing only
+    sv = arg; cv = arg * 0.5f;
+#else
     sincosf(arg, &sv, &cv);
+#endif
     e[2 * t] = sv;
     e[2 * t + 1] = cv;
   }
@@ -679,6 +687,277 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   if (valid && g4 == 0) raw[gs] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
 }
 
+
+// ===========================================================================
+// Training (BASELINE configs[2]): the MLP of a training
+// step as x3 MFMA GEMMs over feature-major activations in HBM ([F][P]: row f
+// holds feature f of every sample p). nerfhip/train_mlp.py chains them:
+//   forward  h_L = act(W_L h_{L-1} + b_L)          x3_layer_kernel (bias, ReLU)
+//   dgrad    d_{L-1} = (W_L^T d_L) * (h_{L-1} > 0)  x3_layer_kernel (W^T, mask)
+//   wgrad    dW_L = d_L h_{L-1}^T (sum over P)      x3_wgrad_kernel (split-K)
+// (network.py:49-74 and its autograd; no reference kernel computes these.)
+// Same 3-term FP16 split as the inference kernel: per-sample activation
+// scales in the layer kernel (K = features), per-tensor scales in wgrad
+// (K = samples: one scale along K).
+// ===========================================================================
+constexpr int kTrainThreads = 512;   // 8 waves x 16 samples
+constexpr int kTrainTile = 128;
+
+__device__ __forceinline__ void vm_wait_slices(int n_pieces) {
+  // wait until at most n_pieces of this wave's LDS-DMA pieces are in flight
+  if (n_pieces >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n_pieces >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n_pieces >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n_pieces >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int G, int NG>
+__device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op& b, Frags& x,
+                                             Frags& y) {
+  if constexpr (G < NG) {
+    lds_drain();
+    if constexpr (G + 1 < NG) {
+      if constexpr ((G & 1) == 0) load_frags<G + 1>(y, base);
+      else load_frags<G + 1>(x, base);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((G & 1) == 0) mfma3x2<false>(acc[2 * G], acc[2 * G + 1], x, b);
+    else mfma3x2<false>(acc[2 * G], acc[2 * G + 1], y, b);
+    __builtin_amdgcn_sched_barrier(0);
+    layer_groups<G + 1, NG>(acc, base, b, x, y);
+  }
+}
+
+// C[m][p] = epi(2^-(sw+e_p) * sum_k W[m][k] * B[k][p]), m < 16*MT, k < 32*NK:
+//   + bias[m] (optional), + ru[m] * rw[p] (optional rank-1 term), ReLU
+//   (optional), * (mask[m][p] > 0) (optional). W packed by pack_x3_matrix
+//   (nerfhip/train_mlp.py): slice q = K step q, block 2t + part = tile t hi/lo,
+//   lane l -> row 16t + (l & 15), k = 32q + 8(l >> 4) + j. One workgroup =
+//   128 samples; W streams L2 -> LDS through a 4-deep ring of slices.
+// epilogue terms, a compile-time set (no per-element branches or waits)
+enum : int { kEpiBias = 1, kEpiRelu = 2, kEpiMask = 4, kEpiRank1 = 8 };
+
+template <int MT, int NK, int EPI>
+__global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
+    const uint4* __restrict__ slices, const int* __restrict__ sw_ptr,
+    const float* __restrict__ bias, const float* __restrict__ B, int64_t ldb,
+    const float* __restrict__ mask, int64_t ldm, const float* __restrict__ ru,
+    const float* __restrict__ rw, float* __restrict__ C, int64_t ldc, int64_t P,
+    float* __restrict__ amax_out) {
+  constexpr int kPieces = 2 * MT;          // 1-KiB LDS-DMA pieces per slice
+  constexpr int kSliceU4 = kPieces * 64;
+  constexpr int kPpw = kPieces / 8;        // pieces per wave
+  static_assert(kPieces % 8 == 0, "MT must be a multiple of 4");
+  __shared__ __attribute__((aligned(16))) uint4 ring[4 * kSliceU4];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g4 = lane >> 4;
+
+  auto stage = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < kPpw; ++i) {
+      const int b = wave + 8 * i;
+      __builtin_amdgcn_global_load_lds((const void*)(slices + (size_t)t * kSliceU4 + b * 64 + lane),
+                                       (lds_ptr_t)(ring + (t & 3) * kSliceU4 + b * 64), 16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (t < NK) stage(t);
+
+  const int64_t p = (int64_t)blockIdx.x * kTrainTile + wave * 16 + (lane & 15);
+  const bool valid = p < P;
+  const int64_t pc = valid ? p : P - 1;   // loads unpredicated (no per-load branches)
+  Op b[NK];
+#pragma unroll
+  for (int q = 0; q < NK; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[q][j] = B[(int64_t)(32 * q + 8 * g4 + j) * ldb + pc];
+#pragma unroll
+  for (int q = 0; q < NK; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[q][j] = valid ? b[q][j] : 0.0f;
+  float mx = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NK; ++q) mx = fmaxf(mx, op_absmax(b[q]));
+  const int e = act_exponent(sample_max(mx));
+  const float s = ldexpf(1.0f, e);
+#pragma unroll
+  for (int q = 0; q < NK; ++q) split_op(b[q], s);
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4(0.0f);
+  __syncthreads();   // prologue slices landed (hipcc waits vmcnt(0) before the barrier)
+
+#pragma unroll
+  for (int q = 0; q < NK; ++q) {
+    if (q + 3 < NK) stage(q + 3);
+    const unsigned base = lds_base((const float*)(ring + (q & 3) * kSliceU4), lane);
+    Frags x, y;
+    load_frags<0>(x, base);
+    layer_groups<0, MT / 2>(acc, base, b[q], x, y);
+    if (q + 1 < NK) {   // slice q+1 landed (this wave's pieces), then visible to all
+      vm_wait_slices(kPpw * ((q + 2 < NK) + (q + 3 < NK)));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  const float inv = ldexpf(1.0f, -(*sw_ptr + e));
+  // epilogue in blocks of 4 tiles: every load of a block issued before its use
+  float omax = 0.0f;   // max |C| of this lane's stored values (for amax_out)
+#pragma unroll
+  for (int t0 = 0; t0 < MT; t0 += 4) {
+    float v[4][4], mk[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * (t0 + t) + 4 * g4 + r;
+        v[t][r] = acc[t0 + t][r] * inv;   // exact: power of two
+        if constexpr ((EPI & kEpiMask) != 0) mk[t][r] = mask[(int64_t)m * ldm + pc];
+        if constexpr ((EPI & kEpiBias) != 0) v[t][r] = v[t][r] + bias[m];
+        if constexpr ((EPI & kEpiRank1) != 0) v[t][r] = __builtin_fmaf(ru[m], rw[pc], v[t][r]);
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr ((EPI & kEpiRelu) != 0) v[t][r] = fmaxf(v[t][r], 0.0f);
+        if constexpr ((EPI & kEpiMask) != 0) v[t][r] = mk[t][r] > 0.0f ? v[t][r] : 0.0f;
+      }
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          C[(int64_t)(16 * (t0 + t) + 4 * g4 + r) * ldc + p] = v[t][r];
+          omax = fmaxf(omax, fabsf(v[t][r]));
+        }
+    }
+  }
+  if (amax_out) {   // one atomic per workgroup (as ordered uint bits: values >= 0)
+    __shared__ unsigned wg_max;
+    if (threadIdx.x == 0) wg_max = 0u;
+    __syncthreads();
+    atomicMax(&wg_max, __float_as_uint(omax));   // LDS atomics
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned*>(amax_out), wg_max);
+  }
+}
+
+// Partial weight gradients: part[c][m][n] = sum over samples p of chunk c of
+// A[m][p] * B[n][p] (A = dL/d(pre-activation) [M][P], B = layer input [N][P],
+// both feature-major). Per-tensor power-of-two scales from amax_a / amax_b
+// (device scalars: max |A|, max |B|) keep the FP16 splits in range; undone
+// exactly at the end. Workgroup tile 128 (m) x 128 (n), K steps of 32 samples
+// staged through LDS already split (hi, lo) in MFMA fragment layout.
+__global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
+    const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
+    int N, int64_t P, int64_t chunk, const float* __restrict__ amax_a,
+    const float* __restrict__ amax_b, float* __restrict__ part, float* __restrict__ bias_part) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][2][16 * 64];   // [stage][A|B][block][lane]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int row = tid >> 2, gq = tid & 3;              // staging unit: row, samples 8gq..8gq+7
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  const int64_t pb = (int64_t)blockIdx.z * chunk;
+  const int64_t pe = pb + chunk < P ? pb + chunk : P;
+  const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
+  const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
+  const bool arow = m0 + row < M, brow = n0 + row < N;
+  const float* ap = A + (int64_t)(arow ? m0 + row : 0) * lda;
+  const float* bp = B + (int64_t)(brow ? n0 + row : 0) * ldb;
+  const int slot = ((row >> 4) * 2) * 64 + (row & 15) + 16 * gq;   // hi block; lo = +64
+
+  auto load8 = [&](const float* src, bool ok, int64_t p0, float (&v)[8]) {
+    if (ok && p0 + 8 <= pe && ((((uintptr_t)(src + p0)) & 15) == 0)) {
+      const float4 u = *reinterpret_cast<const float4*>(src + p0);
+      const float4 w = *reinterpret_cast<const float4*>(src + p0 + 4);
+      v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (ok && p0 + j < pe) ? src[p0 + j] : 0.0f;
+    }
+  };
+  auto put = [&](const float (&v)[8], float sc, uint4* dst) {
+    float hp[4], lp[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) split2(v[2 * k], v[2 * k + 1], sc, hp[k], lp[k]);
+    dst[slot] = make_uint4(__float_as_uint(hp[0]), __float_as_uint(hp[1]), __float_as_uint(hp[2]),
+                           __float_as_uint(hp[3]));
+    dst[slot + 64] = make_uint4(__float_as_uint(lp[0]), __float_as_uint(lp[1]),
+                                __float_as_uint(lp[2]), __float_as_uint(lp[3]));
+  };
+
+  const int mb = wave & 1, nb = wave >> 1;   // wave tile: rows 64mb.., cols 32nb..
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4(0.0f);
+
+  float va[8], vb[8];
+  int st = 0;
+  if (pb < pe) {
+    load8(ap, arow, pb + 8 * gq, va);
+    load8(bp, brow, pb + 8 * gq, vb);
+  }
+  float rsum = 0.0f;   // this thread's share of sum_p A[row][p] (bias gradient)
+  for (int64_t k0 = pb; k0 < pe; k0 += 32) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rsum += va[j];
+    put(va, sa, lds[st][0]);
+    put(vb, sb, lds[st][1]);
+    __syncthreads();
+    if (k0 + 32 < pe) {   // next K step's loads in flight during the MFMAs
+      load8(ap, arow, k0 + 32 + 8 * gq, va);
+      load8(bp, brow, k0 + 32 + 8 * gq, vb);
+    }
+    half8 bh[2], bl[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = 2 * nb + j;
+      bh[j] = __builtin_bit_cast(half8, lds[st][1][(2 * nt) * 64 + lane]);
+      bl[j] = __builtin_bit_cast(half8, lds[st][1][(2 * nt + 1) * 64 + lane]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mt = 4 * mb + i;
+      const half8 ah = __builtin_bit_cast(half8, lds[st][0][(2 * mt) * 64 + lane]);
+      const half8 al = __builtin_bit_cast(half8, lds[st][0][(2 * mt + 1) * 64 + lane]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = MFMA16(ah, bh[j], acc[i][j]);
+        acc[i][j] = MFMA16(ah, bl[j], acc[i][j]);
+        acc[i][j] = MFMA16(al, bh[j], acc[i][j]);
+      }
+    }
+    st ^= 1;   // the other stage is rewritten next step; its readers passed this barrier
+  }
+  if (bias_part && blockIdx.y == 0) {   // the 4 threads of a row are adjacent lanes
+    rsum += __shfl_xor(rsum, 1);
+    rsum += __shfl_xor(rsum, 2);
+    if (gq == 0 && arow) bias_part[(int64_t)blockIdx.z * M + m0 + row] = rsum;
+  }
+  const float inv = ldexpf(1.0f, -(ea + eb));
+  float* out = part + (int64_t)blockIdx.z * M * N;
+  const int g4 = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * (4 * mb + i) + 4 * g4 + r;
+        const int n = n0 + 16 * (2 * nb + j) + (lane & 15);
+        if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][r] * inv;
+      }
+}
+
 }  // namespace nerfhip
 
 using namespace nerfhip;
@@ -700,4 +979,61 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
                      z_stride, total, S, (float4*)raw);
   return check_launch("mlp_x3_kernel");
+}
+
+template <int MT, int NK, int EPI>
+static int launch_layer(const float* w, const int* sw, const float* bias, const float* B,
+                        int64_t ldb, const float* mask, int64_t ldm, const float* ru,
+                        const float* rw, float* C, int64_t ldc, int64_t P, float* amax_out,
+                        nerf_stream_t stream) {
+  hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)cdiv(P, kTrainTile)),
+                     dim3(kTrainThreads), 0, as_stream(stream), (const uint4*)w, sw, bias, B,
+                     ldb, mask, ldm, ru, rw, C, ldc, P, amax_out);
+  return check_launch("x3_layer_kernel");
+}
+
+extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
+                             const float* bias, const float* B, int64_t ldb, const float* mask,
+                             int64_t ldm, const float* ru, const float* rw, int relu, float* C,
+                             int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream) {
+  NERF_REQUIRE(w_packed && w_scale && B && C, "nerf_x3_layer: null pointer");
+  NERF_REQUIRE((ru == nullptr) == (rw == nullptr), "nerf_x3_layer: ru and rw go together");
+  NERF_REQUIRE(P >= 0 && ldb >= P && ldc >= P && (!mask || ldm >= P), "nerf_x3_layer: bad size");
+  NERF_REQUIRE(((uintptr_t)w_packed & 15) == 0, "nerf_x3_layer: packed W must be 16-byte aligned");
+  NERF_REQUIRE(cdiv(P, kTrainTile) < (1ll << 31), "nerf_x3_layer: too many samples");
+  if (P == 0) return 0;
+  const int epi = (bias ? kEpiBias : 0) | (relu ? kEpiRelu : 0) | (mask ? kEpiMask : 0) |
+                  (ru ? kEpiRank1 : 0);
+#define NERF_LAYER_CASE(MT, NK, EPI)                                                          \
+  if (m_tiles == MT && k_steps == NK && epi == (EPI))                                         \
+    return launch_layer<MT, NK, (EPI)>(w_packed, w_scale, bias, B, ldb, mask, ldm, ru, rw, C, \
+                                       ldc, P, amax_out, stream);
+  // forward layers (bias + ReLU; the feature layer without ReLU)
+  NERF_LAYER_CASE(16, 2, kEpiBias | kEpiRelu) NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu)
+  NERF_LAYER_CASE(16, 10, kEpiBias | kEpiRelu) NERF_LAYER_CASE(8, 9, kEpiBias | kEpiRelu)
+  NERF_LAYER_CASE(16, 8, kEpiBias)
+  // backward layers (ReLU mask; + the alpha head's rank-1 term into d h7)
+  NERF_LAYER_CASE(16, 4, 0) NERF_LAYER_CASE(16, 8, kEpiMask)
+  NERF_LAYER_CASE(16, 8, kEpiMask | kEpiRank1) NERF_LAYER_CASE(4, 8, 0)
+  // every term at once (tests)
+  NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiMask | kEpiRank1)
+#undef NERF_LAYER_CASE
+  return fail(NERF_E_UNSUPPORTED, "nerf_x3_layer: unsupported (m_tiles, k_steps, epilogue)");
+}
+
+extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb,
+                             int N, int64_t P, int64_t chunk, const float* amax_a,
+                             const float* amax_b, float* part, float* bias_part,
+                             nerf_stream_t stream) {
+  NERF_REQUIRE(A && B && amax_a && amax_b && part, "nerf_x3_wgrad: null pointer");
+  NERF_REQUIRE(M > 0 && N > 0 && P >= 0 && lda >= P && ldb >= P && chunk > 0 && chunk % 32 == 0,
+               "nerf_x3_wgrad: bad size");
+  const int64_t chunks = cdiv(P, chunk);
+  if (chunks == 0) return 0;
+  NERF_REQUIRE(chunks < 65536, "nerf_x3_wgrad: too many chunks");
+  hipLaunchKernelGGL(x3_wgrad_kernel, dim3((unsigned)cdiv(M, 128), (unsigned)cdiv(N, 128),
+                                           (unsigned)chunks),
+                     dim3(kTrainThreads), 0, as_stream(stream), A, lda, M, B, ldb, N, P, chunk,
+                     amax_a, amax_b, part, bias_part);
+  return check_launch("x3_wgrad_kernel");
 }

@@ -7,12 +7,14 @@ fine-sampling u ~ U[0,1), no detach anywhere), loss = MSE(coarse rgb, target)
 clip_grad_value_(40) (trainers/trainer.py:59), Adam(lr 5e-4, eps 1e-8, no
 weight decay) (src/train/optimizer.py, lego.yaml:63-66, config.py:98).
 
-Division of labour (round 1): the stratified coarse depths come from the HIP
-kernel (bit-exact, no gradient needed); everything differentiable is written
-against torch autograd on the device, with the two 8x256 MLPs as FP32 GEMMs
-(hipBLASLt). Parity with the reference's own forward/backward is pinned by
-tests/golden/t1_train_step.npz. The fused HIP forward+backward is the next
-step.
+Division of labour: the stratified coarse depths come from the HIP kernel
+(bit-exact, no gradient needed); the two 8x256 MLPs run forward and backward
+on the hand-written x3 MFMA kernels (train_mlp.NerfMLPFn: FP32 operands as
+3-term FP16 splits, layer GEMMs over feature-major activations, split-K weight
+gradients); compositing, importance sampling and the loss stay in torch
+autograd around them. mlp="torch" runs the MLPs as torch modules (FP32
+hipBLASLt GEMMs) instead. Parity with the reference's own forward/backward is
+pinned by tests/golden/t1_train_step.npz.
 """
 from __future__ import annotations
 
@@ -80,12 +82,14 @@ def sample_pdf(mids, weights, u):
     return bin_lo + t * (bin_hi - bin_lo)
 
 
-def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True):
+def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query):
     """The differentiable part of a training step (VR:164-194): coarse depths z
     [n, S] (no gradient) -> coarse maps, importance samples from the coarse
-    weights (u [n, N_importance]), fine maps. fine=None: coarse only."""
+    weights (u [n, N_importance]), fine maps. fine=None: coarse only.
+    query_fn(model, pts, dirs) evaluates the MLP (torch module call, or the x3
+    MFMA kernels of train_mlp.query_x3)."""
     pts = rays_o[:, None, :] + rays_d[:, None, :] * z[..., None]
-    raw = query(coarse, pts, rays_d)
+    raw = query_fn(coarse, pts, rays_d)
     rgb0, disp0, acc0, w, depth0 = composite(raw, z, rays_d, white_bkgd)
     out = {"rgb_map_0": rgb0, "disp_map_0": disp0, "acc_map_0": acc0, "depth_map_0": depth0}
     if fine is not None:
@@ -93,7 +97,7 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True):
         zf = sample_pdf(mids, w[..., 1:-1], u)
         z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
         pts2 = rays_o[:, None, :] + rays_d[:, None, :] * z2[..., None]
-        raw2 = query(fine, pts2, rays_d)
+        raw2 = query_fn(fine, pts2, rays_d)
         rgb, disp, acc, _, depth = composite(raw2, z2, rays_d, white_bkgd)
         out.update(rgb_map=rgb, disp_map=disp, acc_map=acc, depth_map=depth)
     return out
@@ -113,7 +117,7 @@ class NerfTrainer:
     """Coarse + fine networks, optimizer and one training step on a ROCm device."""
 
     def __init__(self, device, params, N_samples=64, N_importance=128, near=2.0, far=6.0,
-                 white_bkgd=True, lr=5e-4, clip_value=40.0):
+                 white_bkgd=True, lr=5e-4, clip_value=40.0, mlp="x3"):
         from src.models.nerf.network import NeRF
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -122,6 +126,9 @@ class NerfTrainer:
         self.N_samples, self.N_importance = int(N_samples), int(N_importance)
         self.white_bkgd = bool(white_bkgd)
         self.clip_value = float(clip_value)
+        if mlp not in ("x3", "torch"):
+            raise ValueError("mlp must be 'x3' or 'torch'")
+        self.mlp = mlp
         self.coarse = NeRF().to(self.device)
         self.fine = NeRF().to(self.device)
         self.load(params)
@@ -152,8 +159,10 @@ class NerfTrainer:
         t_rand = t_rand.contiguous()
         call("nerf_sample_coarse", ptr(self.z_base), ptr(t_rand), n, S, ptr(z),
              _lib.stream_of(self.device))
+        from .train_mlp import query_x3
         return render_train(self.coarse, self.fine if self.N_importance > 0 else None,
-                            rays_o, rays_d, z, u, self.white_bkgd)
+                            rays_o, rays_d, z, u, self.white_bkgd,
+                            query_x3 if self.mlp == "x3" else query)
 
     def loss(self, out, target):
         return mse_losses(out, target)

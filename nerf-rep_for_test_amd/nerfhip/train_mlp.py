@@ -1,0 +1,249 @@
+"""The NeRF MLP of a training step on hand-written x3 MFMA kernels.
+
+Forward and backward of ``NeRF.forward`` (src/models/nerf/network.py:49-74:
+8 pts layers with the skip cat(input_pts, h) after layer 4, alpha head,
+feature layer, views layer on cat(feature, input_views), rgb head) for P
+samples, as a ``torch.autograd.Function`` so the rest of the training step
+(compositing, importance sampling, loss; volume_renderer.py:145-357) stays in
+torch autograd around it.
+
+Activations live feature-major in HBM ([F][P]); every 256-wide layer is one
+``nerf_x3_layer`` launch (FP32 operands as 3-term FP16 splits on FP16 MFMA,
+DESIGN.md §3), in both directions:
+
+  forward   h_L = relu(W_L h_{L-1} + b_L)
+  dgrad     d_{L-1} = (W_L^T d_L) * (h_{L-1} > 0)
+  wgrad     dW_L = d_L h_{L-1}^T  (``nerf_x3_wgrad``, split-K partials summed)
+
+The rank-1 heads (alpha 256->1, rgb 128->3), bias gradients (row sums) and
+the frequency encoding with its derivative are small torch ops on the device.
+Weights are repacked from the live parameters every call (device-side torch
+ops, no host sync): packing order = ``pack_x3_matrix``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+XYZ_FREQS, DIR_FREQS = 10, 4
+WGRAD_CHUNK = 1024
+
+
+def freq_encode(x, n_freq):
+    """freq.py:7-32: [x, sin(2^0 x), cos(2^0 x), ..., sin(2^(L-1) x), cos(...)]."""
+    feats = [x]
+    for f in range(n_freq):
+        s = x * float(2 ** f)
+        feats.append(torch.sin(s))
+        feats.append(torch.cos(s))
+    return torch.cat(feats, -1)
+
+
+def pack_x3_matrix(W):
+    """W [M, K] float32 (device; M % 16 == 0, K % 32 == 0) -> (packed FP16 hi/lo
+    fragments as a float32 tensor, int32 [1] scale exponent sw), both on W's
+    device. max|W| * 2^sw lies in [2^11, 2^12). Fragment order: K step q, tile t,
+    part (hi, lo), lane l = r + 16 g, element j = W[16t + r][32q + 8g + j]."""
+    M, K = W.shape
+    assert M % 16 == 0 and K % 32 == 0, (M, K)
+    amax = W.abs().amax()
+    _, ex = torch.frexp(amax)
+    sw = torch.where(amax > 0, 12 - ex, torch.zeros_like(ex)).to(torch.int32).reshape(1)
+    Ws = torch.ldexp(W, sw.to(W.dtype))
+    hi = Ws.half()
+    lo = (Ws - hi.float()).half()
+    fr = torch.stack([hi, lo]).reshape(2, M // 16, 16, K // 32, 4, 8)
+    fr = fr.permute(3, 1, 0, 4, 2, 5).contiguous()        # [q, t, part, g, r, j]
+    return fr.view(torch.float32).reshape(-1), sw
+
+
+def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, rw=None,
+           amax=None):
+    """One nerf_x3_layer launch; amax (a device float, >= 0) is raised to max |C|."""
+    call("nerf_x3_layer", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0), ptr(mask),
+         mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu), ptr(C),
+         C.stride(0), P, ptr(amax), _lib.stream_of(C.device))
+
+
+def _absmax(x):
+    """max |x| as a [1] device tensor (one reduction pass)."""
+    return torch.linalg.vector_norm(x, float("inf")).reshape(1)
+
+
+def _wgrad(A, B, amax_a=None, amax_b=None, with_bias=False):
+    """sum over samples of A[m][p] B[n][p] -> [M, N] (A [M][P], B [N][P]); with_bias:
+    also sum_p A[m][p] -> [M]. amax_a / amax_b: max |A|, max |B| when known."""
+    M, P = A.shape
+    N = B.shape[0]
+    chunks = max(1, -(-P // WGRAD_CHUNK))
+    part = torch.empty((chunks, M, N), device=A.device, dtype=torch.float32)
+    bpart = torch.empty((chunks, M), device=A.device, dtype=torch.float32) if with_bias else None
+    amax_a = _absmax(A) if amax_a is None else amax_a
+    amax_b = _absmax(B) if amax_b is None else amax_b
+    call("nerf_x3_wgrad", ptr(A), A.stride(0), M, ptr(B), B.stride(0), N, P, WGRAD_CHUNK,
+         ptr(amax_a), ptr(amax_b), ptr(part), ptr(bpart), _lib.stream_of(A.device))
+    dw = part.sum(0)
+    return (dw, bpart.sum(0)) if with_bias else dw
+
+
+PARAM_NAMES = ([f"pts_linears.{i}.{k}" for i in range(8) for k in ("weight", "bias")] +
+               ["alpha_linear.weight", "alpha_linear.bias", "feature_linear.weight",
+                "feature_linear.bias", "views_linears.0.weight", "views_linears.0.bias",
+                "rgb_linear.weight", "rgb_linear.bias"])
+
+
+def _padded(W, cols, K):
+    """[M, K] with W's columns at positions `cols` (the rest zero)."""
+    out = torch.zeros((W.shape[0], K), device=W.device, dtype=torch.float32)
+    out[:, cols] = W
+    return out
+
+
+class NerfMLPFn(torch.autograd.Function):
+    """raw [P, 4] = NeRF(cat(freq_encode(pts), freq_encode(dirs))) on x3 kernels.
+    Inputs: pts [P, 3] (gradient returned when it requires one), dirs [P, 3]
+    (no gradient, as in the reference where view directions are constants),
+    then the 24 parameters in PARAM_NAMES order."""
+
+    @staticmethod
+    def forward(ctx, pts, dirs, *params):
+        p = dict(zip(PARAM_NAMES, params))
+        dev = pts.device
+        P = pts.shape[0]
+        f32 = torch.float32
+        enc = freq_encode(pts.detach(), XYZ_FREQS)                  # [P, 63]
+        E = torch.zeros((320, P), device=dev, dtype=f32)           # cat(enc, pad, h4)
+        E[:63] = enc.t()
+        H = [torch.empty((256, P), device=dev, dtype=f32) if i not in (4,) else None
+             for i in range(8)]
+        H[4] = E[64:320]
+        packs = {}
+        for i in range(8):
+            W = p[f"pts_linears.{i}.weight"]
+            if i == 0:
+                W = _padded(W, list(range(63)), 64)
+            elif i == 5:
+                W = _padded(W, list(range(63)) + list(range(64, 320)), 320)
+            packs[i] = pack_x3_matrix(W)
+        # max |.| of every saved activation (the weight-gradient scales): slots
+        # 0-7 = h0..h7 and 8 = feature from the layer kernels, 9 = xyz encoding,
+        # 10 = view encoding
+        amax = torch.zeros(11, device=dev, dtype=f32)
+        src = E[0:64]
+        for i in range(8):
+            wp, sw = packs[i]
+            nk = {0: 2, 5: 10}.get(i, 8)
+            B = E if i == 5 else src
+            _layer(wp, sw, 16, nk, B, H[i], P, bias=p[f"pts_linears.{i}.bias"], relu=True,
+                   amax=amax[i:i + 1])
+            src = H[i]
+        h7 = H[7]
+        alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
+        V = torch.zeros((288, P), device=dev, dtype=f32)           # cat(feature, views enc)
+        wf, swf = pack_x3_matrix(p["feature_linear.weight"])
+        _layer(wf, swf, 16, 8, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
+               amax=amax[8:9])
+        V[256:283] = freq_encode(dirs.detach(), DIR_FREQS).t()
+        amax[9:10] = _absmax(E[:63])
+        amax[10:11] = _absmax(V[256:283])
+        wv, swv = pack_x3_matrix(_padded(p["views_linears.0.weight"], list(range(283)), 288))
+        HV = torch.empty((128, P), device=dev, dtype=f32)
+        _layer(wv, swv, 8, 9, V, HV, P, bias=p["views_linears.0.bias"], relu=True)
+        rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
+        raw = torch.cat([rgb, alpha], 0).t().contiguous()
+        ctx.save_for_backward(pts, E, *H[:4], *H[5:], V, HV, amax, *params)
+        return raw
+
+    @staticmethod
+    def backward(ctx, d_raw):
+        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, *params = ctx.saved_tensors
+        H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
+        p = dict(zip(PARAM_NAMES, params))
+        dev = d_raw.device
+        P = d_raw.shape[0]
+        f32 = torch.float32
+        grads = {}
+        d_raw = d_raw.t().contiguous()                              # [4, P]
+        d_rgb, d_sig = d_raw[0:3], d_raw[3:4]
+        grads["rgb_linear.weight"] = d_rgb @ HV.t()
+        grads["rgb_linear.bias"] = d_rgb.sum(1)
+        d_hv = (p["rgb_linear.weight"].t() @ d_rgb) * (HV > 0)      # [128, P]
+        wv = p["views_linears.0.weight"]                            # [128, 283]
+        gw, gb = _wgrad(d_hv, V, amax_b=torch.maximum(amax[8:9], amax[10:11]), with_bias=True)
+        grads["views_linears.0.weight"] = gw[:, :283]
+        grads["views_linears.0.bias"] = gb
+        dmax = torch.zeros(10, device=dev, dtype=f32)   # max |d| of each layer-kernel output
+        # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
+        wvt, swvt = pack_x3_matrix(wv[:, :256].t().contiguous())
+        DF = torch.empty((256, P), device=dev, dtype=f32)
+        _layer(wvt, swvt, 16, 4, d_hv, DF, P, amax=dmax[8:9])
+        grads["feature_linear.weight"], grads["feature_linear.bias"] = _wgrad(
+            DF, H[7], dmax[8:9], amax[7:8], with_bias=True)
+        grads["alpha_linear.weight"] = d_sig @ H[7].t()
+        grads["alpha_linear.bias"] = d_sig.sum(1)
+        # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
+        wft, swft = pack_x3_matrix(p["feature_linear.weight"].t().contiguous())
+        D = torch.empty((256, P), device=dev, dtype=f32)
+        aw = p["alpha_linear.weight"].reshape(-1).contiguous()
+        dsig = d_sig.reshape(-1).contiguous()
+        _layer(wft, swft, 16, 8, DF, D, P, mask=H[7], ru=aw, rw=dsig, amax=dmax[7:8])
+        d_enc = None
+        for i in range(7, -1, -1):
+            inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
+            in_max = (torch.maximum(amax[9:10], amax[4:5]) if i == 5 else
+                      amax[9:10] if i == 0 else amax[i - 1:i])
+            gw, gb = _wgrad(D, inp, dmax[i:i + 1], in_max, with_bias=True)
+            if i == 0:
+                gw = gw[:, :63]
+            elif i == 5:
+                gw = torch.cat([gw[:, :63], gw[:, 64:320]], 1)
+            grads[f"pts_linears.{i}.weight"] = gw
+            grads[f"pts_linears.{i}.bias"] = gb
+            W = p[f"pts_linears.{i}.weight"]
+            need_enc = pts.requires_grad and ctx.needs_input_grad[0]
+            if i == 0:
+                if need_enc:
+                    wt, swt = pack_x3_matrix(_padded(W, list(range(63)), 64).t().contiguous())
+                    de = torch.empty((64, P), device=dev, dtype=f32)
+                    _layer(wt, swt, 4, 8, D, de, P)
+                    d_enc = de[:63] if d_enc is None else d_enc + de[:63]
+                break
+            if i == 5:
+                Wp = _padded(W, list(range(63)) + list(range(64, 320)), 320).t().contiguous()
+                wt, swt = pack_x3_matrix(Wp[64:320].contiguous())
+                Dn = torch.empty((256, P), device=dev, dtype=f32)
+                _layer(wt, swt, 16, 8, D, Dn, P, mask=H[4], amax=dmax[i - 1:i])
+                if need_enc:
+                    we, swe = pack_x3_matrix(Wp[0:64].contiguous())
+                    de = torch.empty((64, P), device=dev, dtype=f32)
+                    _layer(we, swe, 4, 8, D, de, P)
+                    d_enc = de[:63]
+            else:
+                wt, swt = pack_x3_matrix(W.t().contiguous())
+                Dn = torch.empty((256, P), device=dev, dtype=f32)
+                _layer(wt, swt, 16, 8, D, Dn, P, mask=H[i - 1], amax=dmax[i - 1:i])
+            D = Dn
+        d_pts = None
+        if d_enc is not None:
+            with torch.enable_grad():
+                x = pts.detach().requires_grad_(True)
+                enc = freq_encode(x, XYZ_FREQS)
+                (d_pts,) = torch.autograd.grad(enc, x, d_enc.t())
+        return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
+
+
+def mlp_params(model):
+    """The 24 parameters of a reference NeRF module in PARAM_NAMES order."""
+    named = dict(model.named_parameters())
+    return [named[n] for n in PARAM_NAMES]
+
+
+def query_x3(model, pts, dirs):
+    """Drop-in for train.query (VR:270-284): pts [n, s, 3], dirs [n, 3]."""
+    n, s, _ = pts.shape
+    _lib.require_gpu(pts)
+    d = dirs[:, None, :].expand(n, s, 3).reshape(-1, 3)
+    raw = NerfMLPFn.apply(pts.reshape(-1, 3), d, *mlp_params(model))
+    return raw.reshape(n, s, 4)

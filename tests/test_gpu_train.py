@@ -7,7 +7,9 @@ rgb is compared by PSNR; the gradients of the coarse loss alone to 1e-3, those
 of the full loss by relative norm to 5 % (the fine loss reaches the coarse
 network through the sample positions, where sin(2^9 x) amplifies FP32
 GEMM-order differences; measured worst case 3.7 %, the coarse density bias).
-The same math on the CPU matches the reference to 1e-5 (tests/test_train.py)."""
+The same math on the CPU matches the reference to 1e-5 (tests/test_train.py).
+Both MLP back ends are held to the same bounds: the x3 MFMA kernels
+(train_mlp.py, the default) and torch modules on hipBLASLt FP32 GEMMs."""
 import numpy as np
 import pytest
 import torch
@@ -24,20 +26,21 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _setup(dev):
+def _setup(dev, mlp="x3"):
     from nerfhip.render import NerfPipeline
     from nerfhip.train import NerfTrainer
     z = load("t1_train_step")
     params = params_of(z)
-    tr = NerfTrainer(dev, params)
+    tr = NerfTrainer(dev, params, mlp=mlp)
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128)
     ro, rd = pipe.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
     return z, tr, ro, rd, t(z["t_rand"]), t(z["u"]), t(z["gt"].reshape(-1, 3))
 
 
-def test_forward_loss_and_gradients_match_reference(dev):
-    z, tr, ro, rd, t_rand, u, gt = _setup(dev)
+@pytest.mark.parametrize("mlp", ["x3", "torch"])
+def test_forward_loss_and_gradients_match_reference(dev, mlp):
+    z, tr, ro, rd, t_rand, u, gt = _setup(dev, mlp)
     out = tr.forward(ro, rd, t_rand, u)
     assert max_err(out["rgb_map_0"].detach().cpu().numpy(), z["rgb_map_0"]) < 1e-5
     assert psnr(out["rgb_map"].detach().cpu().numpy(), z["rgb_map"]) > 60.0
@@ -66,8 +69,9 @@ def test_forward_loss_and_gradients_match_reference(dev):
         assert abs(grads[k].norm().item() - ref_norm) <= 5e-2 * ref_norm + 1e-9, k
 
 
-def test_steps_reduce_loss(dev):
-    z, tr, ro, rd, t_rand, u, gt = _setup(dev)
+@pytest.mark.parametrize("mlp", ["x3", "torch"])
+def test_steps_reduce_loss(dev, mlp):
+    z, tr, ro, rd, t_rand, u, gt = _setup(dev, mlp)
     first = tr.step(ro, rd, gt, t_rand, u)["loss"].item()
     for _ in range(30):
         last = tr.step(ro, rd, gt, t_rand, u)["loss"].item()

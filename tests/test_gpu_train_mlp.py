@@ -1,0 +1,134 @@
+"""The x3-MFMA training MLP (nerfhip/train_mlp.py: nerf_x3_layer / nerf_x3_wgrad)
+against the reference NeRF module (network.py:49-74) under torch FP32
+autograd on the same device, on a ragged sample count.
+
+Tolerances (relative to each tensor's max magnitude): forward raw 1e-5;
+parameter gradients and d/d pts 1e-4 (FP32-accurate products, different
+summation order over up to 3000 samples)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda:0")
+
+
+def _model(dev, seed=0, gain=2.0):
+    from nerfhip.synthetic import make_params
+    from src.models.nerf.network import NeRF
+    params = make_params(seed, gain, 0.1)
+    m = NeRF().to(dev)
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            p.copy_(torch.as_tensor(np.asarray(params["model." + k])))
+    return m
+
+
+def _inputs(dev, P, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    pts = (torch.rand((P, 3), generator=g) * 3.0 - 1.5).to(dev)
+    dirs = torch.nn.functional.normalize(torch.randn((P, 3), generator=g), dim=1).to(dev)
+    return pts, dirs
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("P", [1000, 3000])
+def test_x3_train_mlp_forward_backward_match_torch(dev, P):
+    from nerfhip.train import freq_encode
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    m = _model(dev)
+    pts, dirs = _inputs(dev, P)
+    g = torch.Generator(device=dev).manual_seed(2)
+    d_raw = torch.randn((P, 4), device=dev, generator=g)
+
+    # reference: torch FP32 autograd of the reference module
+    x = pts.clone().requires_grad_(True)
+    ref = m(torch.cat([freq_encode(x, 10), freq_encode(dirs, 4)], -1))
+    ref_grads = torch.autograd.grad(ref, [x] + mlp_params(m), d_raw)
+
+    y = pts.clone().requires_grad_(True)
+    out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+    got = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
+    assert _rel(out.detach(), ref.detach()) < 1e-5
+    for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads):
+        assert a.shape == b.shape, name
+        assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+
+
+def test_x3_layer_kernel_matches_matmul(dev):
+    """One nerf_x3_layer launch per supported shape: bias + ReLU + mask + rank-1."""
+    from nerfhip.train_mlp import _layer, pack_x3_matrix
+    g = torch.Generator(device=dev).manual_seed(3)
+    P = 777
+    for mt, nk in [(16, 8)]:       # the all-terms epilogue instance
+        M, K = 16 * mt, 32 * nk
+        W = torch.randn((M, K), device=dev, generator=g) * 0.1
+        B = torch.randn((K, P), device=dev, generator=g) * torch.logspace(-3, 2, P, device=dev)
+        bias = torch.randn(M, device=dev, generator=g)
+        mask = torch.randn((M, P), device=dev, generator=g)
+        ru = torch.randn(M, device=dev, generator=g)
+        rw = torch.randn(P, device=dev, generator=g)
+        wp, sw = pack_x3_matrix(W)
+        C = torch.empty((M, P), device=dev)
+        _layer(wp, sw, mt, nk, B, C, P, bias=bias, relu=True, mask=mask, ru=ru, rw=rw)
+        ref = torch.relu(W.double() @ B.double() + bias.double()[:, None]
+                         + ru.double()[:, None] * rw.double()[None, :]) * (mask > 0)
+        # per sample: the magnitude of every term summed into it
+        scale = (W.double().abs() @ B.double().abs() + bias.double().abs()[:, None]
+                 + ru.double().abs()[:, None] * rw.double().abs()[None, :]).amax(0)
+        err = ((C.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+        assert err < 1e-6, (mt, nk, err)
+
+
+# terms: b = bias, R = ReLU, m = mask, 1 = rank-1 addend
+@pytest.mark.parametrize("mt,nk,terms", [(16, 2, "bR"), (16, 8, "bR"), (16, 10, "bR"),
+                                         (8, 9, "bR"), (16, 8, "b"), (16, 4, ""), (16, 8, "m"),
+                                         (16, 8, "m1"), (4, 8, "")])
+def test_x3_layer_instances(dev, mt, nk, terms):
+    """Every (shape, epilogue) instance the training MLP launches."""
+    from nerfhip.train_mlp import _layer, pack_x3_matrix
+    g = torch.Generator(device=dev).manual_seed(5)
+    P = 300
+    M, K = 16 * mt, 32 * nk
+    W = torch.randn((M, K), device=dev, generator=g) * 0.1
+    B = torch.randn((K, P), device=dev, generator=g)
+    bias = torch.randn(M, device=dev, generator=g) if "b" in terms else None
+    mask = torch.randn((M, P), device=dev, generator=g) if "m" in terms else None
+    ru = torch.randn(M, device=dev, generator=g) if "1" in terms else None
+    rw = torch.randn(P, device=dev, generator=g) if "1" in terms else None
+    wp, sw = pack_x3_matrix(W)
+    C = torch.empty((M, P), device=dev)
+    relu = "R" in terms
+    _layer(wp, sw, mt, nk, B, C, P, bias=bias, relu=relu, mask=mask, ru=ru, rw=rw)
+    ref = W.double() @ B.double()
+    if bias is not None:
+        ref = ref + bias.double()[:, None]
+    if ru is not None:
+        ref = ref + ru.double()[:, None] * rw.double()[None, :]
+    if relu:
+        ref = torch.relu(ref)
+    if mask is not None:
+        ref = ref * (mask > 0)
+    scale = (W.double().abs() @ B.double().abs()).amax(0) + 10.0
+    assert ((C.double() - ref).abs() / scale).max().item() < 1e-6
+
+
+def test_x3_wgrad_matches_matmul(dev):
+    from nerfhip.train_mlp import _wgrad
+    g = torch.Generator(device=dev).manual_seed(4)
+    for M, N, P in [(256, 320, 5000), (128, 288, 4096), (256, 64, 33)]:
+        A = torch.randn((M, P), device=dev, generator=g)
+        B = torch.relu(torch.randn((N, P), device=dev, generator=g))
+        got = _wgrad(A, B).double()
+        ref = A.double() @ B.double().t()
+        scale = (A.double().abs() @ B.double().abs().t()).max().item()
+        assert (got - ref).abs().max().item() / scale < 1e-6, (M, N, P)

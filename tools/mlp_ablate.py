@@ -45,6 +45,7 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_ld4s": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_LOADER_SPLIT=2"],
             # the previous defaults: all 8 waves load (global form), hook VALU after the MFMAs
             "x3_prev": ["-DMLP_DMA_BUF=0", "-DMLP_X3_LOADERS=8", "-DMLP_X3_ILV=0"],
+            "x3_noenc": ["-DABL_NOENC"],
             # hook VALU interleaved into the group's MFMAs, 2 / 4 per gap
             "x3_ilv2": ["-DMLP_X3_ILV=2"], "x3_ilv4": ["-DMLP_X3_ILV=4"],
             "x3_ld4_ilv2": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_ILV=2"]}
