@@ -22,10 +22,19 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 pytestmark = pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc") and
                                 not shutil.which("hipcc"), reason="hipcc not available")
 
-# (file, MFMA mnemonic, count per kernel body): fp32: 2 + 10 + 4x(128) + 64
-# slices' worth; x3: 792 = (2 + 8 + 2) x 48 (layer loop body once) + 4 x 48 + 24
-KERNELS = [("mlp_fused.s", "v_mfma_f32_16x16x4_f32", 2112),
-           ("mlp_x3.s", "v_mfma_f32_16x16x32_f16", 792)]
+# (file, kernel symbol, MFMA mnemonic, count in that kernel's body): fp32:
+# 2 + 10 + 4x(128) + 64 slices' worth; x3: 792 = (2 + 8 + 2) x 48 (layer loop
+# body once) + 4 x 48 + 24
+KERNELS = [("mlp_fused.s", "mlp_fused_kernel", "v_mfma_f32_16x16x4_f32", 2112),
+           ("mlp_x3.s", "mlp_x3_kernel", "v_mfma_f32_16x16x32_f16", 792)]
+
+
+def kernel_body(text, symbol):
+    """The .s text of one kernel: from its label to its .Lfunc_end marker."""
+    m = re.search(r"^(_ZN7nerfhip\d+" + symbol + r"\w*):", text, re.M)
+    assert m, symbol
+    end = text.index(".Lfunc_end", m.end())
+    return text[m.start():end]
 
 
 @pytest.fixture(scope="module")
@@ -35,14 +44,16 @@ def asm_dir():
     return os.path.join(PKG, "build", "asm")
 
 
-@pytest.mark.parametrize("name,mfma,count", KERNELS)
-def test_no_async_lds_hazard(asm_dir, name, mfma, count):
+@pytest.mark.parametrize("name,symbol,mfma,count", KERNELS)
+def test_no_async_lds_hazard(asm_dir, name, symbol, mfma, count):
     import check_async_lds
     assert check_async_lds.main(os.path.join(asm_dir, name)) == 0
 
 
-@pytest.mark.parametrize("name,mfma,count", KERNELS)
-def test_mfma_count_and_no_scratch(asm_dir, name, mfma, count):
+@pytest.mark.parametrize("name,symbol,mfma,count", KERNELS)
+def test_mfma_count_and_no_scratch(asm_dir, name, symbol, mfma, count):
     text = open(os.path.join(asm_dir, name)).read()
-    assert len(re.findall(r"^\s+" + mfma + r"\b", text, re.M)) == count
-    assert re.search(r"\.private_segment_fixed_size:\s+0\b", text)
+    body = kernel_body(text, symbol)
+    assert len(re.findall(r"^\s+" + mfma + r"\b", body, re.M)) == count
+    # no kernel in the file spills
+    assert not re.search(r"\.private_segment_fixed_size:\s+[1-9]", text)
