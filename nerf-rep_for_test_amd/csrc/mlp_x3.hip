@@ -850,110 +850,145 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
 
 // Partial weight gradients: part[c][m][n] = sum over samples p of chunk c of
 // A[m][p] * B[n][p] (A = dL/d(pre-activation) [M][P], B = layer input [N][P],
-// both feature-major). Per-tensor power-of-two scales from amax_a / amax_b
-// (device scalars: max |A|, max |B|) keep the FP16 splits in range; undone
-// exactly at the end. Workgroup tile 128 (m) x 128 (n), K steps of 32 samples
-// staged through LDS already split (hi, lo) in MFMA fragment layout.
+// both feature-major); bias_part[c][m] = sum over the chunk of A[m][p].
+// Per-tensor power-of-two scales from amax_a / amax_b (device scalars: max |A|,
+// max |B|) keep the FP16 splits in range; undone exactly at the end.
+// Workgroup tile 256 (m) x 256 (n): every A and B element of a chunk is read
+// from HBM once. K steps of 32 samples are staged through LDS already split
+// (hi, lo) in MFMA fragment layout, double-buffered, the next step's global
+// loads in flight during the current step's MFMAs. Wave tile 64 x 128: its
+// 4 A fragments stay in registers while the 8 B fragments stream past them.
+constexpr int kWgTile = 256;
 __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
     const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
     int N, int64_t P, int64_t chunk, const float* __restrict__ amax_a,
     const float* __restrict__ amax_b, float* __restrict__ part, float* __restrict__ bias_part) {
-  __shared__ __attribute__((aligned(16))) uint4 lds[2][2][16 * 64];   // [stage][A|B][block][lane]
+  // [stage][A|B][16 tiles x (hi, lo)][64 lanes] x 16 B = 2 x 2 x 32 KiB
+  __shared__ __attribute__((aligned(16))) uint4 lds[2][2][32 * 64];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int row = tid >> 2, gq = tid & 3;              // staging unit: row, samples 8gq..8gq+7
-  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  const int m0 = blockIdx.x * kWgTile, n0 = blockIdx.y * kWgTile;
   const int64_t pb = (int64_t)blockIdx.z * chunk;
   const int64_t pe = pb + chunk < P ? pb + chunk : P;
   const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
-  const bool arow = m0 + row < M, brow = n0 + row < N;
-  const float* ap = A + (int64_t)(arow ? m0 + row : 0) * lda;
-  const float* bp = B + (int64_t)(brow ? n0 + row : 0) * ldb;
-  const int slot = ((row >> 4) * 2) * 64 + (row & 15) + 16 * gq;   // hi block; lo = +64
 
+  // staging units: u = tid + 512 i (i = 0, 1) -> row u >> 2, samples 8 (u & 3) + 0..7
+  const float* ap[2];
+  const float* bp[2];
+  bool aok[2], bok[2];
+  int slot[2], off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int u = tid + 512 * i, row = u >> 2, gq = u & 3;
+    aok[i] = m0 + row < M;
+    bok[i] = n0 + row < N;
+    ap[i] = A + (int64_t)(aok[i] ? m0 + row : 0) * lda;
+    bp[i] = B + (int64_t)(bok[i] ? n0 + row : 0) * ldb;
+    off[i] = 8 * gq;
+    slot[i] = ((row >> 4) * 2) * 64 + (row & 15) + 16 * gq;   // hi block; lo = +64
+  }
   auto load8 = [&](const float* src, bool ok, int64_t p0, float (&v)[8]) {
+    // p0 = this unit's first sample (chunk start + 32 k + 8 gq)
     if (ok && p0 + 8 <= pe && ((((uintptr_t)(src + p0)) & 15) == 0)) {
-      const float4 u = *reinterpret_cast<const float4*>(src + p0);
-      const float4 w = *reinterpret_cast<const float4*>(src + p0 + 4);
-      v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w; v[4] = w.x; v[5] = w.y; v[6] = w.z; v[7] = w.w;
+      const float4 x = *reinterpret_cast<const float4*>(src + p0);
+      const float4 y = *reinterpret_cast<const float4*>(src + p0 + 4);
+      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (ok && p0 + j < pe) ? src[p0 + j] : 0.0f;
     }
   };
-  auto put = [&](const float (&v)[8], float sc, uint4* dst) {
+  auto put = [&](const float (&v)[8], float sc, uint4* dst, int sl) {
     float hp[4], lp[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) split2(v[2 * k], v[2 * k + 1], sc, hp[k], lp[k]);
-    dst[slot] = make_uint4(__float_as_uint(hp[0]), __float_as_uint(hp[1]), __float_as_uint(hp[2]),
-                           __float_as_uint(hp[3]));
-    dst[slot + 64] = make_uint4(__float_as_uint(lp[0]), __float_as_uint(lp[1]),
-                                __float_as_uint(lp[2]), __float_as_uint(lp[3]));
+    dst[sl] = make_uint4(__float_as_uint(hp[0]), __float_as_uint(hp[1]), __float_as_uint(hp[2]),
+                         __float_as_uint(hp[3]));
+    dst[sl + 64] = make_uint4(__float_as_uint(lp[0]), __float_as_uint(lp[1]),
+                              __float_as_uint(lp[2]), __float_as_uint(lp[3]));
   };
 
-  const int mb = wave & 1, nb = wave >> 1;   // wave tile: rows 64mb.., cols 32nb..
-  f32x4 acc[4][2];
+  const int mb = wave & 3, nb = wave >> 2;   // wave tile: rows 64 mb.., cols 128 nb..
+  const bool busy = (m0 + 64 * mb < M) && (n0 + 128 * nb < N);   // wave-uniform
+  f32x4 acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4(0.0f);
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.0f);
 
-  float va[8], vb[8];
+  float va[2][8], vb[2][8];
+  float rsum[2] = {0.0f, 0.0f};   // shares of sum_p A[row][p] (bias gradient)
   int st = 0;
   if (pb < pe) {
-    load8(ap, arow, pb + 8 * gq, va);
-    load8(bp, brow, pb + 8 * gq, vb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      load8(ap[i], aok[i], pb + off[i], va[i]);
+      load8(bp[i], bok[i], pb + off[i], vb[i]);
+    }
   }
-  float rsum = 0.0f;   // this thread's share of sum_p A[row][p] (bias gradient)
   for (int64_t k0 = pb; k0 < pe; k0 += 32) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rsum += va[j];
-    put(va, sa, lds[st][0]);
-    put(vb, sb, lds[st][1]);
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rsum[i] += va[i][j];
+      put(va[i], sa, lds[st][0], slot[i]);
+      put(vb[i], sb, lds[st][1], slot[i]);
+    }
     __syncthreads();
     if (k0 + 32 < pe) {   // next K step's loads in flight during the MFMAs
-      load8(ap, arow, k0 + 32 + 8 * gq, va);
-      load8(bp, brow, k0 + 32 + 8 * gq, vb);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        load8(ap[i], aok[i], k0 + 32 + off[i], va[i]);
+        load8(bp[i], bok[i], k0 + 32 + off[i], vb[i]);
+      }
     }
-    half8 bh[2], bl[2];
+    if (busy) {
+      half8 ah[4], al[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int nt = 2 * nb + j;
-      bh[j] = __builtin_bit_cast(half8, lds[st][1][(2 * nt) * 64 + lane]);
-      bl[j] = __builtin_bit_cast(half8, lds[st][1][(2 * nt + 1) * 64 + lane]);
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int mt = 4 * mb + i;
+        ah[i] = __builtin_bit_cast(half8, lds[st][0][(2 * mt) * 64 + lane]);
+        al[i] = __builtin_bit_cast(half8, lds[st][0][(2 * mt + 1) * 64 + lane]);
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int mt = 4 * mb + i;
-      const half8 ah = __builtin_bit_cast(half8, lds[st][0][(2 * mt) * 64 + lane]);
-      const half8 al = __builtin_bit_cast(half8, lds[st][0][(2 * mt + 1) * 64 + lane]);
+      for (int j = 0; j < 8; ++j) {
+        const int nt = 8 * nb + j;
+        const half8 bh = __builtin_bit_cast(half8, lds[st][1][(2 * nt) * 64 + lane]);
+        const half8 bl = __builtin_bit_cast(half8, lds[st][1][(2 * nt + 1) * 64 + lane]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[i][j] = MFMA16(ah, bh[j], acc[i][j]);
-        acc[i][j] = MFMA16(ah, bl[j], acc[i][j]);
-        acc[i][j] = MFMA16(al, bh[j], acc[i][j]);
+        for (int i = 0; i < 4; ++i) {
+          acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
+          acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
+          acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
+        }
       }
     }
     st ^= 1;   // the other stage is rewritten next step; its readers passed this barrier
   }
   if (bias_part && blockIdx.y == 0) {   // the 4 threads of a row are adjacent lanes
-    rsum += __shfl_xor(rsum, 1);
-    rsum += __shfl_xor(rsum, 2);
-    if (gq == 0 && arow) bias_part[(int64_t)blockIdx.z * M + m0 + row] = rsum;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float r = rsum[i];
+      r += __shfl_xor(r, 1);
+      r += __shfl_xor(r, 2);
+      const int u = tid + 512 * i;
+      if ((u & 3) == 0 && aok[i]) bias_part[(int64_t)blockIdx.z * M + m0 + (u >> 2)] = r;
+    }
   }
+  if (!busy) return;
   const float inv = ldexpf(1.0f, -(ea + eb));
   float* out = part + (int64_t)blockIdx.z * M * N;
   const int g4 = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 16 * (4 * mb + i) + 4 * g4 + r;
-        const int n = n0 + 16 * (2 * nb + j) + (lane & 15);
+        const int m = m0 + 64 * mb + 16 * i + 4 * g4 + r;
+        const int n = n0 + 128 * nb + 16 * j + (lane & 15);
         if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][r] * inv;
       }
 }
@@ -1031,7 +1066,7 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
   const int64_t chunks = cdiv(P, chunk);
   if (chunks == 0) return 0;
   NERF_REQUIRE(chunks < 65536, "nerf_x3_wgrad: too many chunks");
-  hipLaunchKernelGGL(x3_wgrad_kernel, dim3((unsigned)cdiv(M, 128), (unsigned)cdiv(N, 128),
+  hipLaunchKernelGGL(x3_wgrad_kernel, dim3((unsigned)cdiv(M, kWgTile), (unsigned)cdiv(N, kWgTile),
                                            (unsigned)chunks),
                      dim3(kTrainThreads), 0, as_stream(stream), A, lda, M, B, ldb, N, P, chunk,
                      amax_a, amax_b, part, bias_part);

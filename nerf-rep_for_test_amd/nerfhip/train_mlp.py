@@ -28,7 +28,12 @@ from . import _lib
 from ._lib import call, ptr
 
 XYZ_FREQS, DIR_FREQS = 10, 4
-WGRAD_CHUNK = 1024
+
+
+def wgrad_chunk(P):
+    """Samples per weight-gradient workgroup: about 256 chunks (one workgroup per
+    CU for a 256x256 output), a multiple of 32 in [256, 4096]."""
+    return min(4096, max(256, -(-P // (256 * 32)) * 32))
 
 
 def freq_encode(x, n_freq):
@@ -77,12 +82,13 @@ def _wgrad(A, B, amax_a=None, amax_b=None, with_bias=False):
     also sum_p A[m][p] -> [M]. amax_a / amax_b: max |A|, max |B| when known."""
     M, P = A.shape
     N = B.shape[0]
-    chunks = max(1, -(-P // WGRAD_CHUNK))
+    chunk = wgrad_chunk(P)
+    chunks = max(1, -(-P // chunk))
     part = torch.empty((chunks, M, N), device=A.device, dtype=torch.float32)
     bpart = torch.empty((chunks, M), device=A.device, dtype=torch.float32) if with_bias else None
     amax_a = _absmax(A) if amax_a is None else amax_a
     amax_b = _absmax(B) if amax_b is None else amax_b
-    call("nerf_x3_wgrad", ptr(A), A.stride(0), M, ptr(B), B.stride(0), N, P, WGRAD_CHUNK,
+    call("nerf_x3_wgrad", ptr(A), A.stride(0), M, ptr(B), B.stride(0), N, P, chunk,
          ptr(amax_a), ptr(amax_b), ptr(part), ptr(bpart), _lib.stream_of(A.device))
     dw = part.sum(0)
     return (dw, bpart.sum(0)) if with_bias else dw
