@@ -104,6 +104,12 @@ int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_
 int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                   int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
                   float* part, float* bias_part, nerf_stream_t stream);
+/* nerf_x3_pack: packs n weight matrices for nerf_x3_layer in one launch. descs
+ * (device) = n records {const float* src; int64_t ldr, ldc; const int* rowmap;
+ * const int* colmap; int M, K; void* out; int* sw} (64 bytes each): padded
+ * element (i, k) = src[rowmap[i]*ldr + colmap[k]*ldc] (0 where a map entry is
+ * -1); out receives the FP16 (hi, lo) fragments, *sw the scale exponent. */
+int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream);
 
 /* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
  * Reductions follow torch's CPU float32 summation order.

@@ -993,6 +993,63 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
       }
 }
 
+
+// Packing of the training MLP's weight matrices for x3_layer_kernel, all of a
+// network in one launch (one workgroup per matrix): padded element (i, k) =
+// src[rowmap[i] * ldr + colmap[k] * ldc] (0 where a map is -1), scaled by 2^sw
+// with max|W| * 2^sw in [2^11, 2^12), split into FP16 (hi, lo) fragments
+// [q][t][part][g][r][j] = element (16t + r, 32q + 8g + j) (nerfhip.train_mlp).
+struct X3PackDesc {
+  const float* src;
+  int64_t ldr, ldc;
+  const int* rowmap;
+  const int* colmap;
+  int M, K;
+  uint4* out;
+  int* sw;
+};
+
+__global__ __launch_bounds__(1024) void x3_pack_kernel(const X3PackDesc* __restrict__ descs) {
+  const X3PackDesc d = descs[blockIdx.x];
+  const int tid = threadIdx.x;
+  __shared__ unsigned wg_max;
+  if (tid == 0) wg_max = 0u;
+  __syncthreads();
+  float mx = 0.0f;
+  for (int idx = tid; idx < d.M * d.K; idx += 1024) {
+    const int ri = d.rowmap[idx / d.K], ck = d.colmap[idx % d.K];
+    if (ri >= 0 && ck >= 0) mx = fmaxf(mx, fabsf(d.src[ri * d.ldr + ck * d.ldc]));
+  }
+  atomicMax(&wg_max, __float_as_uint(mx));
+  __syncthreads();
+  const float amax = __uint_as_float(wg_max);
+  int E = 0;
+  if (amax > 0.0f) (void)frexpf(amax, &E);
+  const int sw = amax > 0.0f ? 12 - E : 0;
+  if (tid == 0) *d.sw = sw;
+  const float scale = ldexpf(1.0f, sw);
+  const int mt = d.M / 16;
+  const int groups = (d.K / 32) * mt * 64;   // (q, t, lane) -> 8 halfs hi + 8 halfs lo
+  for (int gi = tid; gi < groups; gi += 1024) {
+    const int lane = gi & 63, qt = gi >> 6;
+    const int q = qt / mt, t = qt - q * mt;
+    const int row = 16 * t + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
+    const int ri = d.rowmap[row];
+    half8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ck = d.colmap[k0 + j];
+      const float v = (ri >= 0 && ck >= 0) ? d.src[ri * d.ldr + ck * d.ldc] * scale : 0.0f;
+      const _Float16 h = (_Float16)v;
+      hi[j] = h;
+      lo[j] = (_Float16)(v - (float)h);
+    }
+    const int blk = (q * mt + t) * 2;
+    d.out[blk * 64 + lane] = __builtin_bit_cast(uint4, hi);
+    d.out[(blk + 1) * 64 + lane] = __builtin_bit_cast(uint4, lo);
+  }
+}
+
 }  // namespace nerfhip
 
 using namespace nerfhip;
@@ -1071,4 +1128,12 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
                      dim3(kTrainThreads), 0, as_stream(stream), A, lda, M, B, ldb, N, P, chunk,
                      amax_a, amax_b, part, bias_part);
   return check_launch("x3_wgrad_kernel");
+}
+
+extern "C" int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream) {
+  NERF_REQUIRE(descs && n >= 0 && n < 65536, "nerf_x3_pack: bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)n), dim3(1024), 0, as_stream(stream),
+                     (const X3PackDesc*)descs);
+  return check_launch("x3_pack_kernel");
 }

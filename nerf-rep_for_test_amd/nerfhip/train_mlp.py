@@ -64,6 +64,88 @@ def pack_x3_matrix(W):
     return fr.view(torch.float32).reshape(-1), sw
 
 
+class X3Packer:
+    """All 21 weight matrices of one network's training step (forward W and
+    backward W^T, padded as the layer kernels need them) packed by ONE
+    nerf_x3_pack launch from the live parameters; the output buffers, index
+    maps and descriptor table are built once and reused while the parameters
+    keep their storage (the optimizer updates them in place).
+
+    Entries: name -> (param, transposed, rowmap, colmap); the padded matrix's
+    element (i, k) is param[rowmap[i]][colmap[k]] (param^T when transposed)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.key = None
+
+    @staticmethod
+    def plan(p):
+        ar = lambda n: list(range(n))   # noqa: E731
+        enc64 = ar(63) + [-1]
+        plan = {"fwd0": ("pts_linears.0.weight", False, ar(256), enc64),
+                "fwd5": ("pts_linears.5.weight", False, ar(256), enc64 + list(range(63, 319))),
+                "fwd_feat": ("feature_linear.weight", False, ar(256), ar(256)),
+                "fwd_views": ("views_linears.0.weight", False, ar(128), ar(283) + [-1] * 5),
+                "bwd_views": ("views_linears.0.weight", True, ar(256), ar(128)),
+                "bwd_feat": ("feature_linear.weight", True, ar(256), ar(256)),
+                "bwd5h": ("pts_linears.5.weight", True, list(range(63, 319)), ar(256)),
+                "bwd5e": ("pts_linears.5.weight", True, enc64, ar(256)),
+                "bwd0": ("pts_linears.0.weight", True, enc64, ar(256))}
+        for i in (1, 2, 3, 4, 6, 7):
+            plan[f"fwd{i}"] = (f"pts_linears.{i}.weight", False, ar(256), ar(256))
+            plan[f"bwd{i}"] = (f"pts_linears.{i}.weight", True, ar(256), ar(256))
+        return plan
+
+    def _build(self, p):
+        import numpy as np
+        plan = self.plan(p)
+        dev = self.device
+        self.names = list(plan)
+        self.out, self.maps, recs = {}, [], []
+        self.sw = torch.zeros(len(plan), device=dev, dtype=torch.int32)
+        for n, (pname, tr, rmap, cmap) in enumerate(plan.values()):
+            W = p[pname]
+            M, K = len(rmap), len(cmap)
+            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
+            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
+            self.maps += [rm, cm]
+            out = torch.empty(M * K, device=dev, dtype=torch.float32)   # M*K halfs x 2
+            self.out[self.names[n]] = (out, M // 16, K // 32)
+            ldr, ldc = (W.stride(0), W.stride(1)) if not tr else (W.stride(1), W.stride(0))
+            recs.append((W.data_ptr(), ldr, ldc, rm.data_ptr(), cm.data_ptr(), M, K,
+                         out.data_ptr(), self.sw[n:n + 1].data_ptr()))
+        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
+                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
+                       ("sw", "<u8")])
+        assert dt.itemsize == 64
+        table = np.array(recs, dtype=dt)
+        self.table = torch.from_numpy(table.view(np.uint8).copy()).to(dev)
+
+    def pack(self, p):
+        """p: parameter name -> tensor. Returns name -> (packed, sw [1], m_tiles, k_steps)."""
+        key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()) if k.endswith("weight"))
+        if key != self.key:
+            self._build(p)
+            self.key = key
+        call("nerf_x3_pack", ptr(self.table), len(self.names), _lib.stream_of(self.device))
+        return {n: (o, self.sw[i:i + 1], mt, nk)
+                for i, (n, (o, mt, nk)) in enumerate(self.out.items())}
+
+
+_PACKERS = {}
+
+
+def _packs_for(params, device):
+    """Packed matrices of the network whose weight tensors these are (one packer
+    per network, keyed by the first weight's storage)."""
+    p = dict(zip(PARAM_NAMES, params))
+    key = p["pts_linears.0.weight"].data_ptr()
+    pk = _PACKERS.get(key)
+    if pk is None:
+        pk = _PACKERS[key] = X3Packer(device)
+    return pk.pack(p)
+
+
 def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, rw=None,
            amax=None):
     """One nerf_x3_layer launch; amax (a device float, >= 0) is raised to max |C|."""
@@ -125,41 +207,34 @@ class NerfMLPFn(torch.autograd.Function):
         H = [torch.empty((256, P), device=dev, dtype=f32) if i not in (4,) else None
              for i in range(8)]
         H[4] = E[64:320]
-        packs = {}
-        for i in range(8):
-            W = p[f"pts_linears.{i}.weight"]
-            if i == 0:
-                W = _padded(W, list(range(63)), 64)
-            elif i == 5:
-                W = _padded(W, list(range(63)) + list(range(64, 320)), 320)
-            packs[i] = pack_x3_matrix(W)
+        pk = _packs_for(params, dev)
         # max |.| of every saved activation (the weight-gradient scales): slots
         # 0-7 = h0..h7 and 8 = feature from the layer kernels, 9 = xyz encoding,
         # 10 = view encoding
         amax = torch.zeros(11, device=dev, dtype=f32)
         src = E[0:64]
         for i in range(8):
-            wp, sw = packs[i]
-            nk = {0: 2, 5: 10}.get(i, 8)
+            wp, sw, mt, nk = pk[f"fwd{i}"]
             B = E if i == 5 else src
-            _layer(wp, sw, 16, nk, B, H[i], P, bias=p[f"pts_linears.{i}.bias"], relu=True,
+            _layer(wp, sw, mt, nk, B, H[i], P, bias=p[f"pts_linears.{i}.bias"], relu=True,
                    amax=amax[i:i + 1])
             src = H[i]
         h7 = H[7]
         alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
         V = torch.zeros((288, P), device=dev, dtype=f32)           # cat(feature, views enc)
-        wf, swf = pack_x3_matrix(p["feature_linear.weight"])
-        _layer(wf, swf, 16, 8, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
+        wf, swf, mt, nk = pk["fwd_feat"]
+        _layer(wf, swf, mt, nk, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
                amax=amax[8:9])
         V[256:283] = freq_encode(dirs.detach(), DIR_FREQS).t()
         amax[9:10] = _absmax(E[:63])
         amax[10:11] = _absmax(V[256:283])
-        wv, swv = pack_x3_matrix(_padded(p["views_linears.0.weight"], list(range(283)), 288))
+        wv, swv, mt, nk = pk["fwd_views"]
         HV = torch.empty((128, P), device=dev, dtype=f32)
-        _layer(wv, swv, 8, 9, V, HV, P, bias=p["views_linears.0.bias"], relu=True)
+        _layer(wv, swv, mt, nk, V, HV, P, bias=p["views_linears.0.bias"], relu=True)
         rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
         raw = torch.cat([rgb, alpha], 0).t().contiguous()
         ctx.save_for_backward(pts, E, *H[:4], *H[5:], V, HV, amax, *params)
+        ctx.packs = pk
         return raw
 
     @staticmethod
@@ -167,6 +242,7 @@ class NerfMLPFn(torch.autograd.Function):
         pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, *params = ctx.saved_tensors
         H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
         p = dict(zip(PARAM_NAMES, params))
+        pk = ctx.packs
         dev = d_raw.device
         P = d_raw.shape[0]
         f32 = torch.float32
@@ -182,15 +258,15 @@ class NerfMLPFn(torch.autograd.Function):
         grads["views_linears.0.bias"] = gb
         dmax = torch.zeros(10, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
-        wvt, swvt = pack_x3_matrix(wv[:, :256].t().contiguous())
+        wvt, swvt, mt, nk = pk["bwd_views"]
         DF = torch.empty((256, P), device=dev, dtype=f32)
-        _layer(wvt, swvt, 16, 4, d_hv, DF, P, amax=dmax[8:9])
+        _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
         grads["feature_linear.weight"], grads["feature_linear.bias"] = _wgrad(
             DF, H[7], dmax[8:9], amax[7:8], with_bias=True)
         grads["alpha_linear.weight"] = d_sig @ H[7].t()
         grads["alpha_linear.bias"] = d_sig.sum(1)
         # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
-        wft, swft = pack_x3_matrix(p["feature_linear.weight"].t().contiguous())
+        wft, swft, _, _ = pk["bwd_feat"]
         D = torch.empty((256, P), device=dev, dtype=f32)
         aw = p["alpha_linear.weight"].reshape(-1).contiguous()
         dsig = d_sig.reshape(-1).contiguous()
@@ -207,29 +283,26 @@ class NerfMLPFn(torch.autograd.Function):
                 gw = torch.cat([gw[:, :63], gw[:, 64:320]], 1)
             grads[f"pts_linears.{i}.weight"] = gw
             grads[f"pts_linears.{i}.bias"] = gb
-            W = p[f"pts_linears.{i}.weight"]
             need_enc = pts.requires_grad and ctx.needs_input_grad[0]
             if i == 0:
                 if need_enc:
-                    wt, swt = pack_x3_matrix(_padded(W, list(range(63)), 64).t().contiguous())
+                    wt, swt, mt, nk = pk["bwd0"]
                     de = torch.empty((64, P), device=dev, dtype=f32)
-                    _layer(wt, swt, 4, 8, D, de, P)
+                    _layer(wt, swt, mt, nk, D, de, P)
                     d_enc = de[:63] if d_enc is None else d_enc + de[:63]
                 break
+            Dn = torch.empty((256, P), device=dev, dtype=f32)
             if i == 5:
-                Wp = _padded(W, list(range(63)) + list(range(64, 320)), 320).t().contiguous()
-                wt, swt = pack_x3_matrix(Wp[64:320].contiguous())
-                Dn = torch.empty((256, P), device=dev, dtype=f32)
-                _layer(wt, swt, 16, 8, D, Dn, P, mask=H[4], amax=dmax[i - 1:i])
+                wt, swt, mt, nk = pk["bwd5h"]
+                _layer(wt, swt, mt, nk, D, Dn, P, mask=H[4], amax=dmax[i - 1:i])
                 if need_enc:
-                    we, swe = pack_x3_matrix(Wp[0:64].contiguous())
+                    we, swe, mt, nk = pk["bwd5e"]
                     de = torch.empty((64, P), device=dev, dtype=f32)
-                    _layer(we, swe, 4, 8, D, de, P)
+                    _layer(we, swe, mt, nk, D, de, P)
                     d_enc = de[:63]
             else:
-                wt, swt = pack_x3_matrix(W.t().contiguous())
-                Dn = torch.empty((256, P), device=dev, dtype=f32)
-                _layer(wt, swt, 16, 8, D, Dn, P, mask=H[i - 1], amax=dmax[i - 1:i])
+                wt, swt, mt, nk = pk[f"bwd{i}"]
+                _layer(wt, swt, mt, nk, D, Dn, P, mask=H[i - 1], amax=dmax[i - 1:i])
             D = Dn
         d_pts = None
         if d_enc is not None:

@@ -132,3 +132,25 @@ def test_x3_wgrad_matches_matmul(dev):
         ref = A.double() @ B.double().t()
         scale = (A.double().abs() @ B.double().abs().t()).max().item()
         assert (got - ref).abs().max().item() / scale < 1e-6, (M, N, P)
+
+
+def test_x3_packer_matches_reference_packing(dev):
+    """The one-launch packer (nerf_x3_pack) == pack_x3_matrix of each padded matrix."""
+    from nerfhip.train_mlp import PARAM_NAMES, X3Packer, mlp_params, pack_x3_matrix
+    m = _model(dev)
+    p = dict(zip(PARAM_NAMES, mlp_params(m)))
+    packer = X3Packer(dev)
+    got = packer.pack(p)
+    for name, (pname, tr, rmap, cmap) in X3Packer.plan(p).items():
+        W = p[pname].detach()
+        W = W.t() if tr else W
+        Wp = torch.zeros((len(rmap), len(cmap)), device=dev)
+        ri = torch.tensor(rmap, device=dev)
+        ci = torch.tensor(cmap, device=dev)
+        ok = (ri[:, None] >= 0) & (ci[None, :] >= 0)
+        Wp[ok] = W[ri.clamp_min(0)][:, ci.clamp_min(0)][ok]
+        ref, sw = pack_x3_matrix(Wp)
+        out, sw_got, mt, nk = got[name]
+        assert (mt, nk) == (len(rmap) // 16, len(cmap) // 32), name
+        assert int(sw_got.item()) == int(sw.item()), name
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32)), name
