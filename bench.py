@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--checkpoint", default=None,
                     help="trained weights (a reference-format .pth or model dir) instead of "
                          "the synthetic generator")
+    ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
+                    help="c3: the MLPs on the x3 MFMA training kernels (default) or as torch "
+                         "modules (FP32 hipBLASLt GEMMs)")
     ap.add_argument("--no-fp32-run", action="store_true",
                     help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
     args = ap.parse_args()
@@ -198,7 +201,7 @@ def bench_train(args, world, rank, dev, params, data, barrier):
     poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
     K = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32,
                      device=dev)
-    tr = NerfTrainer(dev, params)
+    tr = NerfTrainer(dev, params, mlp=args.train_mlp)
     group = dist.group.WORLD if world > 1 else None
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     nrays = 1024
@@ -232,21 +235,39 @@ def bench_train(args, world, rank, dev, params, data, barrier):
         "value": nrays * world * args.steps / elapsed / 1e6, "unit": "Mrays/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": data + ", synthetic targets",
+        "vs_baseline": None,
+        "dtype": DTYPES["f16x3"] if args.train_mlp == "x3" else "fp32",
+        "data": data + ", synthetic targets",
         "config": {"workload": "lego train step: 1024 random pixels of the test cameras per "
                                "rank, perturb 1, training-mode u, MSE coarse+fine, clip 40, Adam",
                    "baseline_config": "configs[2]", "N_rays": nrays, "N_samples": 64,
-                   "N_importance": 128, "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
-        "roofline": {"bound": "mfma", "kernel": "whole step (MLP GEMMs on hipBLASLt dominate)",
-                     "achieved": flop / step_s / 1e12, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": flop / step_s / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-                     "traffic": None, "flop_per_step": flop},
+                   "N_importance": 128, "train_mlp": args.train_mlp,
+                   "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
+        "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def train_roofline(mlp, flop, step_s):
+    """C3: the whole step's algorithmic MLP FLOP/s (fwd + 2x bwd) against the MFMA
+    peak of the arithmetic the MLP GEMMs run on (x3: 3 FP16 MFMA products per
+    FP32 product; torch: FP32 hipBLASLt)."""
+    algo = flop / step_s / 1e12
+    if mlp == "x3":
+        kernel, achieved, peak, unit = ("whole step (x3_layer_kernel + x3_wgrad_kernel dominate)",
+                                        3 * algo, FP16_MFMA_PEAK_TFLOPS,
+                                        "TFLOP/s (FP16 MFMA, 3 per FP32 product)")
+    else:
+        kernel, achieved, peak, unit = ("whole step (MLP GEMMs on hipBLASLt dominate)", algo,
+                                        FP32_MFMA_PEAK_TFLOPS, "TFLOP/s")
+    return {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": achieved / peak, "algorithmic_tflops": algo,
+            "frac_of_fp32_peak": algo / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+            "flop_per_step": flop}
 
 
 DTYPES = {"fp32": "fp32",

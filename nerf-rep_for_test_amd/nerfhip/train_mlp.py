@@ -202,8 +202,9 @@ class NerfMLPFn(torch.autograd.Function):
         P = pts.shape[0]
         f32 = torch.float32
         enc = freq_encode(pts.detach(), XYZ_FREQS)                  # [P, 63]
-        E = torch.zeros((320, P), device=dev, dtype=f32)           # cat(enc, pad, h4)
+        E = torch.empty((320, P), device=dev, dtype=f32)           # cat(enc, pad, h4)
         E[:63] = enc.t()
+        E[63].zero_()                                              # h4 rows: layer 4
         H = [torch.empty((256, P), device=dev, dtype=f32) if i not in (4,) else None
              for i in range(8)]
         H[4] = E[64:320]
@@ -221,7 +222,8 @@ class NerfMLPFn(torch.autograd.Function):
             src = H[i]
         h7 = H[7]
         alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
-        V = torch.zeros((288, P), device=dev, dtype=f32)           # cat(feature, views enc)
+        V = torch.empty((288, P), device=dev, dtype=f32)           # cat(feature, views enc)
+        V[283:].zero_()                                            # feature rows: its layer
         wf, swf, mt, nk = pk["fwd_feat"]
         _layer(wf, swf, mt, nk, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
                amax=amax[8:9])
@@ -249,7 +251,7 @@ class NerfMLPFn(torch.autograd.Function):
         grads = {}
         d_raw = d_raw.t().contiguous()                              # [4, P]
         d_rgb, d_sig = d_raw[0:3], d_raw[3:4]
-        grads["rgb_linear.weight"] = d_rgb @ HV.t()
+        grads["rgb_linear.weight"] = _wgrad(d_rgb, HV)            # K = P: x3 split-K GEMM
         grads["rgb_linear.bias"] = d_rgb.sum(1)
         d_hv = (p["rgb_linear.weight"].t() @ d_rgb) * (HV > 0)      # [128, P]
         wv = p["views_linears.0.weight"]                            # [128, 283]
@@ -263,7 +265,7 @@ class NerfMLPFn(torch.autograd.Function):
         _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
         grads["feature_linear.weight"], grads["feature_linear.bias"] = _wgrad(
             DF, H[7], dmax[8:9], amax[7:8], with_bias=True)
-        grads["alpha_linear.weight"] = d_sig @ H[7].t()
+        grads["alpha_linear.weight"] = _wgrad(d_sig, H[7], amax_b=amax[7:8])
         grads["alpha_linear.bias"] = d_sig.sum(1)
         # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
         wft, swft, _, _ = pk["bwd_feat"]
