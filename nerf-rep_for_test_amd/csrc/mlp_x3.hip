@@ -733,10 +733,31 @@ __device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op
 //   + bias[m] (optional), + ru[m] * rw[p] (optional rank-1 term), ReLU
 //   (optional), * (mask[m][p] > 0) (optional). W packed by pack_x3_matrix
 //   (nerfhip/train_mlp.py): slice q = K step q, block 2t + part = tile t hi/lo,
-//   lane l -> row 16t + (l & 15), k = 32q + 8(l >> 4) + j. One workgroup =
-//   128 samples; W streams L2 -> LDS through a 4-deep ring of slices.
+//   lane l -> row 16t + (l & 15), k = 32q + 8(l >> 4) + j.
+// Persistent: a workgroup walks sample tiles of 128 (tile, tile + gridDim.x,
+// ...); W streams L2 -> LDS through a 4-deep ring of slices that runs on
+// across tiles, and after slice q of a tile the registers of its B operand are
+// refilled with K step q of the NEXT tile, so those HBM loads land while the
+// rest of the tile computes. Each tile ends with vmcnt(0): within a tile the
+// counted wait before a slice barrier then only counts that tile's operations.
 // epilogue terms, a compile-time set (no per-element branches or waits)
 enum : int { kEpiBias = 1, kEpiRelu = 2, kEpiMask = 4, kEpiRank1 = 8 };
+
+__device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n uniform
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
 
 template <int MT, int NK, int EPI>
 __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
@@ -753,90 +774,151 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g4 = lane >> 4;
+  const int64_t ntiles = (P + kTrainTile - 1) / kTrainTile;
+  const int64_t t0 = blockIdx.x, tstride = gridDim.x;
+  const int nt = t0 < ntiles ? (int)((ntiles - 1 - t0) / tstride + 1) : 0;   // this WG's tiles
+  const int total = nt * NK;                                                  // its slices
 
-  auto stage = [&](int t) {
+  // slice g of this workgroup's stream = K step g % NK, in ring slot g & 3;
+  // buffer-form LDS-DMA: the lane offset is constant, the slice offset an SGPR
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)slices, 0, NK * kSliceU4 * 16, 0x00020000);
+  auto stage = [&](int g) {
+    if (g < total) {
+      const int q = g % NK;
 #pragma unroll
-    for (int i = 0; i < kPpw; ++i) {
-      const int b = wave + 8 * i;
-      __builtin_amdgcn_global_load_lds((const void*)(slices + (size_t)t * kSliceU4 + b * 64 + lane),
-                                       (lds_ptr_t)(ring + (t & 3) * kSliceU4 + b * 64), 16, 0, 0);
+      for (int i = 0; i < kPpw; ++i) {
+        const int b = wave + 8 * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rW, (lds_ptr_t)(ring + (g & 3) * kSliceU4 + b * 64), 16, (b * 64 + lane) * 16,
+            __builtin_amdgcn_readfirstlane(q * kSliceU4 * 16), 0, 0);
+      }
     }
   };
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-    if (t < NK) stage(t);
+  stage(0);
+  stage(1);
+  stage(2);
 
-  const int64_t p = (int64_t)blockIdx.x * kTrainTile + wave * 16 + (lane & 15);
-  const bool valid = p < P;
-  const int64_t pc = valid ? p : P - 1;   // loads unpredicated (no per-load branches)
+  auto sample_of = [&](int64_t tile) {
+    return tile * kTrainTile + wave * 16 + (lane & 15);
+  };
+  // HBM operands as buffer resources: a lane's offset is one 32-bit VGPR, the
+  // row offset an SGPR, and a sample past P reads 0 / drops its store (offset
+  // pushed past num_records) -- no per-load address registers or branches
+  const int nbB = (int)(32 * NK * ldb * 4), nbC = (int)(16 * MT * ldc * 4);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, nbC, 0x00020000);
+  const int nbM = mask ? (int)(16 * MT * ldm * 4) : 0;
+  const __amdgpu_buffer_rsrc_t rM =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(mask ? mask : B), 0, nbM, 0x00020000);
+  // row 32 q + 8 g4 + j of sample p: VGPR offset (8 g4 + j) rows + p (8 per
+  // lane, one per j), SGPR offset 32 q rows (one per K step)
+  const unsigned ldb4 = (unsigned)ldb * 4u;
+  struct VOff { unsigned o[8]; };
+  auto voff_b = [&](int64_t p) {
+    VOff v;
+    const unsigned base = p < P ? (unsigned)(((int64_t)8 * g4 * ldb + p) * 4) : (unsigned)nbB;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v.o[j] = base + (unsigned)j * ldb4;
+    return v;
+  };
+  auto load_b = [&](int q, const VOff& vo, Op& dst) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      dst[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rB, (int)vo.o[j], (int)(32u * q * ldb4), 0));
+  };
   Op b[NK];
+  {
+    const VOff vo = voff_b(sample_of(t0));
 #pragma unroll
-  for (int q = 0; q < NK; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[q][j] = B[(int64_t)(32 * q + 8 * g4 + j) * ldb + pc];
-#pragma unroll
-  for (int q = 0; q < NK; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[q][j] = valid ? b[q][j] : 0.0f;
-  float mx = 0.0f;
-#pragma unroll
-  for (int q = 0; q < NK; ++q) mx = fmaxf(mx, op_absmax(b[q]));
-  const int e = act_exponent(sample_max(mx));
-  const float s = ldexpf(1.0f, e);
-#pragma unroll
-  for (int q = 0; q < NK; ++q) split_op(b[q], s);
-
-  f32x4 acc[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = f32x4(0.0f);
+    for (int q = 0; q < NK; ++q) load_b(q, vo, b[q]);
+  }
   __syncthreads();   // prologue slices landed (hipcc waits vmcnt(0) before the barrier)
 
-#pragma unroll
-  for (int q = 0; q < NK; ++q) {
-    if (q + 3 < NK) stage(q + 3);
-    const unsigned base = lds_base((const float*)(ring + (q & 3) * kSliceU4), lane);
-    Frags x, y;
-    load_frags<0>(x, base);
-    layer_groups<0, MT / 2>(acc, base, b[q], x, y);
-    if (q + 1 < NK) {   // slice q+1 landed (this wave's pieces), then visible to all
-      vm_wait_slices(kPpw * ((q + 2 < NK) + (q + 3 < NK)));
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  const float inv = ldexpf(1.0f, -(*sw_ptr + e));
-  // epilogue in blocks of 4 tiles: every load of a block issued before its use
+  const int sw = *sw_ptr;
   float omax = 0.0f;   // max |C| of this lane's stored values (for amax_out)
+  int g = 0;
+  for (int it = 0; it < nt; ++it) {
+    const int64_t tile = t0 + (int64_t)it * tstride;
+    const int64_t p = sample_of(tile);
+    const bool valid = p < P;
+    const int64_t pc = valid ? p : P - 1;
+    const bool has_next = it + 1 < nt;
+    const VOff von = voff_b(sample_of(tile + tstride));
+    float mx = 0.0f;   // (samples past P loaded as 0)
 #pragma unroll
-  for (int t0 = 0; t0 < MT; t0 += 4) {
-    float v[4][4], mk[4][4];
+    for (int q = 0; q < NK; ++q) mx = fmaxf(mx, op_absmax(b[q]));
+    const int e = act_exponent(sample_max(mx));
+    const float s = ldexpf(1.0f, e);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int q = 0; q < NK; ++q) split_op(b[q], s);
+
+    f32x4 acc[MT];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * (t0 + t) + 4 * g4 + r;
-        v[t][r] = acc[t0 + t][r] * inv;   // exact: power of two
-        if constexpr ((EPI & kEpiMask) != 0) mk[t][r] = mask[(int64_t)m * ldm + pc];
-        if constexpr ((EPI & kEpiBias) != 0) v[t][r] = v[t][r] + bias[m];
-        if constexpr ((EPI & kEpiRank1) != 0) v[t][r] = __builtin_fmaf(ru[m], rw[pc], v[t][r]);
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4(0.0f);
+
+#pragma unroll
+    for (int q = 0; q < NK; ++q, ++g) {
+      stage(g + 3);
+      const unsigned base = lds_base((const float*)(ring + (g & 3) * kSliceU4), lane);
+      Frags x, y;
+      load_frags<0>(x, base);
+      layer_groups<0, MT / 2>(acc, base, b[q], x, y);
+      if (has_next) load_b(q, von, b[q]);   // K step q of the next tile, registers just freed
+      if (g + 1 < total) {   // slice g+1 landed (this wave's pieces), then visible to all
+        if (q >= 2) {
+          // younger than the pieces of g+1 (issued at slice q-2 of this tile): the
+          // next-tile loads of slices q-2..q and the pieces of g+2, g+3
+          vm_wait_n(24 * (int)has_next + kPpw * ((g + 2 < total) + (g + 3 < total)));
+        }   // q < 2: those pieces were issued before this tile's closing vmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
       }
+    }
+
+    const float inv = ldexpf(1.0f, -(sw + e));
+    // row 16 t + 4 g4 + r: VGPR offset (4 g4 + r) rows + p, SGPR offset 16 t rows
+    const unsigned ldc4 = (unsigned)ldc * 4u, ldm4 = (unsigned)ldm * 4u;
+    unsigned voc[4], vom[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int r = 0; r < 4; ++r) {
+      voc[r] = valid ? (unsigned)(((int64_t)(4 * g4 + r) * ldc + p) * 4) : (unsigned)nbC;
+      vom[r] = valid ? (unsigned)(((int64_t)(4 * g4 + r) * ldm + p) * 4) : (unsigned)nbM;
+    }
+    // epilogue in blocks of 4 tiles: every load of a block issued before its use
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr ((EPI & kEpiRelu) != 0) v[t][r] = fmaxf(v[t][r], 0.0f);
-        if constexpr ((EPI & kEpiMask) != 0) v[t][r] = mk[t][r] > 0.0f ? v[t][r] : 0.0f;
-      }
-    if (valid) {
+    for (int u0 = 0; u0 < MT; u0 += 4) {
+      float v[4][4], mk[4][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          C[(int64_t)(16 * (t0 + t) + 4 * g4 + r) * ldc + p] = v[t][r];
-          omax = fmaxf(omax, fabsf(v[t][r]));
+          const int m = 16 * (u0 + t) + 4 * g4 + r;
+          v[t][r] = acc[u0 + t][r] * inv;   // exact: power of two
+          if constexpr ((EPI & kEpiMask) != 0)
+            mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rM, (int)vom[r], (int)(16u * (u0 + t) * ldm4), 0));
+          if constexpr ((EPI & kEpiBias) != 0) v[t][r] = v[t][r] + bias[m];
+          if constexpr ((EPI & kEpiRank1) != 0) v[t][r] = __builtin_fmaf(ru[m], rw[pc], v[t][r]);
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr ((EPI & kEpiRelu) != 0) v[t][r] = fmaxf(v[t][r], 0.0f);
+          if constexpr ((EPI & kEpiMask) != 0) v[t][r] = mk[t][r] > 0.0f ? v[t][r] : 0.0f;
+        }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // a sample past P: offset past num_records, dropped
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[t][r]), rC,
+                                                (int)voc[r], (int)(16u * (u0 + t) * ldc4), 0);
+          omax = valid ? fmaxf(omax, fabsf(v[t][r])) : omax;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile starts clean
   }
   if (amax_out) {   // one atomic per workgroup (as ordered uint bits: values >= 0)
     __shared__ unsigned wg_max;
@@ -1078,7 +1160,9 @@ static int launch_layer(const float* w, const int* sw, const float* bias, const 
                         int64_t ldb, const float* mask, int64_t ldm, const float* ru,
                         const float* rw, float* C, int64_t ldc, int64_t P, float* amax_out,
                         nerf_stream_t stream) {
-  hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)cdiv(P, kTrainTile)),
+  // persistent: at most 256 workgroups (one per CU: the ring takes 64-128 KiB of LDS)
+  const int64_t tiles = cdiv(P, kTrainTile);
+  hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)(tiles < 256 ? tiles : 256)),
                      dim3(kTrainThreads), 0, as_stream(stream), (const uint4*)w, sw, bias, B,
                      ldb, mask, ldm, ru, rw, C, ldc, P, amax_out);
   return check_launch("x3_layer_kernel");
@@ -1093,6 +1177,9 @@ extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_ti
   NERF_REQUIRE(P >= 0 && ldb >= P && ldc >= P && (!mask || ldm >= P), "nerf_x3_layer: bad size");
   NERF_REQUIRE(((uintptr_t)w_packed & 15) == 0, "nerf_x3_layer: packed W must be 16-byte aligned");
   NERF_REQUIRE(cdiv(P, kTrainTile) < (1ll << 31), "nerf_x3_layer: too many samples");
+  NERF_REQUIRE(128ll * k_steps * ldb < (1ll << 31) && 64ll * m_tiles * ldc < (1ll << 31) &&
+                   (!mask || 64ll * m_tiles * ldm < (1ll << 31)),
+               "nerf_x3_layer: an operand spans 2 GiB or more (32-bit buffer offsets)");
   if (P == 0) return 0;
   const int epi = (bias ? kEpiBias : 0) | (relu ? kEpiRelu : 0) | (mask ? kEpiMask : 0) |
                   (ru ? kEpiRank1 : 0);
