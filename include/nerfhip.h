@@ -94,9 +94,11 @@ int nerf_mlp_forward_x3(const float* w_slices, const float* w_head,
  *   instances are those the training MLP launches (nerf-rep_for_test_amd/csrc/
  *   mlp_x3.hip); others return NERF_E_UNSUPPORTED. amax_out (optional, device
  *   float, caller-initialised) is raised to max |C|.
- * nerf_x3_wgrad: part[c][m][n] = sum over samples p in [c*chunk, (c+1)*chunk)
- *   of A[m][p] * B[n][p]; amax_a / amax_b = device max|A|, max|B|; bias_part
- *   (optional) [c][m] = sum over the chunk's samples of A[m][p]. */
+ * nerf_x3_wgrad: part[c][m][n] = sum over the samples p of subset c of
+ *   A[m][p] * B[n][p], for C = ceil(P / chunk) subsets (subset c = 32-sample
+ *   steps c, c+C, c+2C, ...: their sum over c is the full product);
+ *   amax_a / amax_b = device max|A|, max|B|; bias_part (optional) [c][m] =
+ *   the same subsets' sums of A[m][p]. */
 int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
                   const float* bias, const float* B, int64_t ldb, const float* mask,
                   int64_t ldm, const float* ru, const float* rw, int relu, float* C,

@@ -930,7 +930,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
   }
 }
 
-// Partial weight gradients: part[c][m][n] = sum over samples p of chunk c of
+// Partial weight gradients: part[c][m][n] = sum over the samples of subset c
+// (32-sample steps c, c + C, c + 2C, ... of C = ceil(P / chunk) subsets) of
 // A[m][p] * B[n][p] (A = dL/d(pre-activation) [M][P], B = layer input [N][P],
 // both feature-major); bias_part[c][m] = sum over the chunk of A[m][p].
 // Per-tensor power-of-two scales from amax_a / amax_b (device scalars: max |A|,
@@ -951,8 +952,13 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int m0 = blockIdx.x * kWgTile, n0 = blockIdx.y * kWgTile;
-  const int64_t pb = (int64_t)blockIdx.z * chunk;
-  const int64_t pe = pb + chunk < P ? pb + chunk : P;
+  // K steps of 32 samples interleaved over the gridDim.z workgroups of an output
+  // tile (step z, z + Z, ...): the concurrently running workgroups read
+  // neighbouring samples of every row (DRAM page locality)
+  const int64_t pb = (int64_t)blockIdx.z * 32;
+  const int64_t pe = P;
+  const int64_t kstride = (int64_t)gridDim.z * 32;
+  (void)chunk;
   const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
 
@@ -1010,7 +1016,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
       load8(bp[i], bok[i], pb + off[i], vb[i]);
     }
   }
-  for (int64_t k0 = pb; k0 < pe; k0 += 32) {
+  for (int64_t k0 = pb; k0 < pe; k0 += kstride) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -1019,11 +1025,11 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
       put(vb[i], sb, lds[st][1], slot[i]);
     }
     __syncthreads();
-    if (k0 + 32 < pe) {   // next K step's loads in flight during the MFMAs
+    if (k0 + kstride < pe) {   // next K step's loads in flight during the MFMAs
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        load8(ap[i], aok[i], k0 + 32 + off[i], va[i]);
-        load8(bp[i], bok[i], k0 + 32 + off[i], vb[i]);
+        load8(ap[i], aok[i], k0 + kstride + off[i], va[i]);
+        load8(bp[i], bok[i], k0 + kstride + off[i], vb[i]);
       }
     }
     if (busy) {
