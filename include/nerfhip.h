@@ -48,6 +48,9 @@ int nerf_version(void);                 /* ABI version, bumped on layout changes
 #define NERF_MLP_SLICES 73
 #define NERF_MLP_SLICE_FLOATS 8192
 #define NERF_MLP_HEAD_FLOATS 3200
+/* nerf_mlp_forward_x3's packing (nerfhip.pack.pack_mlp_x3) folds the
+ * activation-free feature layer into the views layer: 65 slices. */
+#define NERF_MLP_X3_SLICES 65
 
 /* VR:115-143: camera rays for pixels [p0, p0+n) of an H x W image (row-major,
  * pixel p -> (y = p / W, x = p % W), integer pixel centres), origin = pose

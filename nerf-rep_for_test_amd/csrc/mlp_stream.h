@@ -57,15 +57,16 @@ struct Dma {
   int live;
 };
 
-// blocks b0.. of slice t of the packed network at `slices` (t >= kSlices or
-// !live: nothing to stage)
+// blocks b0.. of slice t of a packed network of nslices slices at `slices`
+// (t >= nslices or !live: nothing to stage)
 __device__ __forceinline__ Dma make_dma_blocks(const float4* slices, int t, float* buf, int b0,
-                                               int wave, int lane, bool live) {
+                                               int wave, int lane, bool live,
+                                               int nslices = kSlices) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)slices, 0, kSlices * kSliceFloats * 4, 0x00020000);
+      (void*)slices, 0, nslices * kSliceFloats * 4, 0x00020000);
   return Dma{r, (unsigned)__builtin_amdgcn_readfirstlane(t * kSliceFloats * 4),
              (unsigned)((b0 * 64 + lane) * 16), buf + b0 * 256, wave,
-             __builtin_amdgcn_readfirstlane(live && t < kSlices ? 1 : 0)};
+             __builtin_amdgcn_readfirstlane(live && t < nslices ? 1 : 0)};
 }
 
 // slice t of the packed network at `slices` (t >= kSlices: nothing to stage)

@@ -43,6 +43,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 // the FP16 hi halves (VGPRs 0-3) and lo halves (VGPRs 4-7) after it.
 typedef f32x8 Op;
 
+// The x3 stream folds the feature layer into the views layer (pack_mlp_x3,
+// fold_feature_into_views): 65 slices instead of the FP32 kernel's 73.
+constexpr int kX3Slices = NERF_MLP_X3_SLICES;
 constexpr int kX3Threads = 64 * kStreamWaves;
 constexpr int kX3Tile = 16 * kStreamWaves;
 
@@ -146,9 +149,10 @@ constexpr int kX3Pieces = MLP_X3_LOADERS == 4 ? 8 : 4;   // per loading wave and
 __device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane) {
 #if MLP_X3_LOADERS == 4
   static_assert(MLP_DMA_BUF, "4 loader waves need the buffer-form DMA");
-  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4);
+  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4, kX3Slices);
 #else
-  return make_dma(slices, t, buf, wave, lane);
+  static_assert(MLP_DMA_BUF, "the x3 stream (kX3Slices) needs the buffer-form DMA");
+  return make_dma_blocks(slices, t, buf, wave * kBlocksPerWave, wave, lane, true, kX3Slices);
 #endif
 }
 
@@ -606,9 +610,11 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 
   float alpha = 0.0f;
   // ---- layers 1..7 (skip input at 5) + feature (8, no ReLU) ----------------
-  for (int L = 1; L <= 8; ++L) {
-    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)),
-                L != 8 ? 0.0f : -__builtin_inff(), lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
+  // (the feature layer, NET:63, has no activation: pack_mlp_x3 folds it into the
+  // views layer, which then reads h7 directly)
+  for (int L = 1; L <= 7; ++L) {
+    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)), 0.0f,
+                lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
                 L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
     act_slices(acc, R, g, X, s, fp, epi);
     g += 8;
@@ -624,7 +630,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     // the next layer's input scale (the skip layer's covers the encoding too)
     float mx = epi.amax;
     if (L == 4) mx = fmaxf(mx, enc_max);
-    if (L == 8) break;
+    if (L == 7) break;
     e = act_exponent(sample_max(mx));
     s = ldexpf(1.0f, e);
     split_op(X[0], s);
@@ -633,9 +639,10 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
       split_op(encf[1], s);
     }
   }
-  // acc holds zeros; X holds the feature layer (FP32, unsplit)
+  // acc holds zeros; X holds h7 (FP32, unsplit)
 
-  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67) -
+  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67),
+  // with feature = W_f h7 + b_f folded in: W_views,feat W_f on h7 ------------
   Op dirf;
   encode_dir(dv, g4, dirf);
   {

@@ -315,18 +315,43 @@ def _x3_frags(Ws, cols, tiles):
     return np.stack([h, lo], 2)
 
 
+X3_SLICES = 65   # SLICES minus the feature layer's 8 (folded into the views layer)
+
+
+def fold_feature_into_views(Wf, bf, Wv, bv):
+    """The feature layer has no activation (network.py:63-66: feature =
+    feature_linear(h); h = views_linears(cat(feature, input_views))), so
+    W_v [feat | dir] . cat(W_f h + b_f, d) + b_v = (W_v,feat W_f) h + W_v,dir d
+    + (W_v,feat b_f + b_v): one [128 x (256 + 27)] layer on h7 instead of a
+    256x256 layer and the views layer. Products in float64, rounded once to
+    float32 (the reference rounds feature to float32 instead: both are within
+    FP32 rounding of the exact map). Returns (W [128, 283], b [128])."""
+    Wf, bf, Wv, bv = (np.asarray(a, np.float64) for a in (Wf, bf, Wv, bv))
+    W = np.concatenate([Wv[:, :256] @ Wf, Wv[:, 256:]], 1)
+    b = Wv[:, :256] @ bf + bv
+    return W.astype(np.float32), b.astype(np.float32)
+
+
 def pack_mlp_x3(params, prefix="model"):
-    """Packed network for nerf_mlp_forward_x3: (slices float32[73*8192] holding
-    FP16 fragment pairs, head float32[3200])."""
+    """Packed network for nerf_mlp_forward_x3: (slices float32[65*8192] holding
+    FP16 fragment pairs, head float32[3200]). The feature layer is folded into
+    the views layer (fold_feature_into_views): 11 % fewer MACs per sample."""
     def get(name):
         v = params[f"{prefix}.{name}"]
         v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
         return np.ascontiguousarray(v, np.float32)
 
     _, head = pack_mlp(params, prefix)          # biases and VALU heads: same layout
+    Wc, bc = fold_feature_into_views(get("feature_linear.weight"), get("feature_linear.bias"),
+                                     get("views_linears.0.weight"), get("views_linears.0.bias"))
+    head[H_BIAS_VIEWS:H_BIAS_VIEWS + 128] = _group_pack(bc, 8).reshape(-1)
+    head[H_BIAS + 8 * 256:H_BIAS + 9 * 256] = 0.0   # feature bias: folded
     slices = []
     for li, (name, kind, tiles) in enumerate(layer_plan()):
-        Wt = get(name + ".weight")
+        if name == "feature_linear":
+            head[H_SCALES + li] = 0
+            continue
+        Wt = Wc if name == "views_linears.0" else get(name + ".weight")
         sw = weight_exponent(Wt)
         head[H_SCALES + li] = sw
         cols = _x3_layer_cols(kind)
@@ -341,13 +366,13 @@ def pack_mlp_x3(params, prefix="model"):
                 for qq in range(min(2, fr.shape[0] - q0)):
                     blk[16 * qq:16 * qq + 16] = fr[q0 + qq].reshape(16, 64, 8)
                 slices.append(blk)
-    assert len(slices) == SLICES, len(slices)
+    assert len(slices) == X3_SLICES, len(slices)
     allh = np.stack(slices).reshape(-1)
     return np.ascontiguousarray(allh).view(np.float32).copy(), head
 
 
 def _x3_decode(slices):
-    return slices.view(np.float16).reshape(SLICES, 32, 64, 8).astype(np.float64)
+    return slices.view(np.float16).reshape(X3_SLICES, 32, 64, 8).astype(np.float64)
 
 
 def emulate_x3(slices, head, pts, dirs):
@@ -393,7 +418,7 @@ def emulate_x3(slices, head, pts, dirs):
     h = np.maximum(acc * 2.0 ** -(hd[H_SCALES] + e) + bias_of(H_BIAS, 16)[:, None], 0)
     g = 2
     alpha = None
-    for L in range(1, 9):
+    for L in range(1, 8):                         # the feature layer is folded into views
         x = h.T                                   # [P, 256] features
         mx = np.abs(x).max(1)
         if L == 5:
@@ -407,8 +432,7 @@ def emulate_x3(slices, head, pts, dirs):
             acc += mm([g, g + 1], [0, 0], Eh, El, 16)
             g += 2
         h = acc * 2.0 ** -(hd[H_SCALES + L] + e) + bias_of(H_BIAS + L * 256, 16)[:, None]
-        if L != 8:
-            h = np.maximum(h, 0)
+        h = np.maximum(h, 0)
         if L == 7:
             aw = _group_pack_inv(hd[H_ALPHA_W:H_ALPHA_W + 256], 16)
             alpha = aw @ h + hd[H_ALPHA_B]

@@ -3,7 +3,7 @@ emulation of its MFMA dataflow, reproduces the oracle MLP (CPU only)."""
 import numpy as np
 import pytest
 
-from nerfhip.pack import (H_SCALES, HEAD_FLOATS, SLICE_FLOATS, SLICES, col_act, emulate,
+from nerfhip.pack import (H_SCALES, HEAD_FLOATS, SLICE_FLOATS, SLICES, X3_SLICES, col_act, emulate,
                           emulate_x3, pack_mlp, pack_mlp_x3, x3_cols_act, x3_cols_dir,
                           x3_cols_enc)
 from nerfhip.synthetic import make_params
@@ -46,7 +46,7 @@ def test_x3_packed_network_matches_oracle(seed, gain, prefix):
     in FP16's normal range)."""
     p = make_params(seed, gain, 1.0)
     sl, hd = pack_mlp_x3(p, prefix)
-    assert sl.shape == (SLICES * SLICE_FLOATS,) and hd.shape == (HEAD_FLOATS,)
+    assert sl.shape == (X3_SLICES * SLICE_FLOATS,) and hd.shape == (HEAD_FLOATS,)
     assert np.all(hd[H_SCALES:H_SCALES + 10] >= 0)
     rng = np.random.default_rng(seed)
     pts = rng.uniform(-2, 2, (65, 3)).astype(np.float32)
