@@ -1089,6 +1089,150 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 }
 
 
+// The same partial weight gradients for aligned operands (host-checked: P a
+// multiple of 32, 16-B aligned rows, operands < 2 GiB): the raw FP32 K steps
+// land in LDS by buffer-form LDS-DMA, so no registers hold in-flight data and
+// step k+1's 64 KiB (A and B rows of 32 samples) stream in during all of step
+// k's work; each wave splits the fragments it reads (FP32 -> FP16 hi/lo) in
+// registers. LDS: 2 stages x 64 pieces of 1 KiB; piece (o, t, h) = operand o
+// (A, B), 16-row tile t, half h: lane l holds row 16t + (l & 15), samples
+// 8 (l >> 4) + 4h .. +3, so the two halves read by lane l are one MFMA
+// fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past M / N read 0
+// (offset past num_records). Bias sums from the A fragments (waves nb = 0).
+__global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
+    const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
+    int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
+    float* __restrict__ part, float* __restrict__ bias_part) {
+  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
+  const int m0 = blockIdx.x * kWgTile, n0 = blockIdx.y * kWgTile;
+  const int64_t pb = (int64_t)blockIdx.z * 32, kstride = (int64_t)gridDim.z * 32;
+  const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
+  const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
+
+  // this wave's 8 pieces per step: q = 8 wave + i (waves 0-3: A, 4-7: B)
+  const bool opb = wave >= 4;
+  const int nbA = (int)((int64_t)M * lda * 4), nbB = (int)((int64_t)N * ldb * 4);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(opb ? B : A), 0, opb ? nbB : nbA, 0x00020000);
+  unsigned vo[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = (8 * wave + i) & 31, t = q >> 1, h = q & 1;
+    const int row = (opb ? n0 : m0) + 16 * t + (lane & 15);
+    const int64_t ld = opb ? ldb : lda;
+    vo[i] = row < (opb ? N : M) ? (unsigned)(((int64_t)row * ld + 8 * (lane >> 4) + 4 * h) * 4)
+                               : (unsigned)(opb ? nbB : nbA);
+  }
+  auto issue = [&](int64_t k, int s) {
+    const int so = __builtin_amdgcn_readfirstlane((int)(k * 4));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(&stg[s][(8 * wave + i) * 64]), 16,
+                                               (int)vo[i], so, 0, 0);
+  };
+
+  const int mb = wave & 3, nb = wave >> 2;   // wave tile: rows 64 mb.., cols 128 nb..
+  const bool busy = (m0 + 64 * mb < M) && (n0 + 128 * nb < N);   // wave-uniform
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.0f);
+  float rs4[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's share of sum_p A (nb = 0)
+
+  // the raw FP32 fragment of a tile: its two pieces (halves), 2 KiB apart per tile
+  // Raw: the two halves as the asm wrote them. A drain names every pending Raw
+  // as an in/out operand, so no copy or shuffle of one can run before it lands.
+  struct Raw { u32x4 x, y; };
+  auto read_pair = [&](unsigned addr, Raw& r) {   // addr: LDS byte address of half 0
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r.x) : "v"(addr) : "memory");
+    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(r.y) : "v"(addr) : "memory");
+  };
+  auto to_op = [](const Raw& r) {
+    return __builtin_bit_cast(Op, __builtin_shufflevector(r.x, r.y, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  if (pb < P) issue(pb, 0);
+  int s = 0;
+  for (int64_t k0 = pb; k0 < P; k0 += kstride, s ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of step k0
+    __builtin_amdgcn_s_barrier();   // everyone's landed; stage s^1's readers are done
+    asm volatile("" ::: "memory");
+    if (k0 + kstride < P) issue(k0 + kstride, s ^ 1);
+    if (busy) {
+      const unsigned base = lds_addr((const float*)&stg[s][0]) + lane * 16u;
+      half8 ah[4], al[4];
+      {
+        Raw ra[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) read_pair(base + (unsigned)((4 * mb + i) * 2048), ra[i]);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
+                       "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y)
+                     :
+                     : "memory");
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          Op v = to_op(ra[i]);
+          if (nb == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rs4[i] += v[j];
+          }
+          split_op(v, sa);
+          ah[i] = op_hi(v);
+          al[i] = op_lo(v);
+        }
+      }
+      Raw rb[2];
+      // B tile nt = 8 nb + j: pieces 32 + 2 nt, + 1
+      read_pair(base + (unsigned)((16 + 8 * nb) * 2048), rb[0]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Raw& cur = rb[j & 1];
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
+        Op b = to_op(cur);
+        if (j + 1 < 8) read_pair(base + (unsigned)((16 + 8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
+        split_op(b, sb);
+        const half8 bh = op_hi(b), bl = op_lo(b);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
+          acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
+          acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
+        }
+      }
+    }
+  }
+  if (bias_part && blockIdx.y == 0 && nb == 0 && busy) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // row 16 (4 mb + i) + (l & 15): lanes l, l^16, l^32, l^48
+      float r = rs4[i];
+      r += __shfl_xor(r, 16);
+      r += __shfl_xor(r, 32);
+      const int row = m0 + 16 * (4 * mb + i) + lane;
+      if (lane < 16 && row < M) bias_part[(int64_t)blockIdx.z * M + row] = r;
+    }
+  }
+  if (!busy) return;
+  const float inv = ldexpf(1.0f, -(ea + eb));
+  float* out = part + (int64_t)blockIdx.z * M * N;
+  const int g4 = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 64 * mb + 16 * i + 4 * g4 + r;
+        const int n = n0 + 128 * nb + 16 * j + (lane & 15);
+        if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][r] * inv;
+      }
+}
+
+
 // Packing of the training MLP's weight matrices for x3_layer_kernel, all of a
 // network in one launch (one workgroup per matrix): padded element (i, k) =
 // src[rowmap[i] * ldr + colmap[k] * ldc] (0 where a map is -1), scaled by 2^sw
@@ -1223,10 +1367,17 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
   const int64_t chunks = cdiv(P, chunk);
   if (chunks == 0) return 0;
   NERF_REQUIRE(chunks < 65536, "nerf_x3_wgrad: too many chunks");
-  hipLaunchKernelGGL(x3_wgrad_kernel, dim3((unsigned)cdiv(M, kWgTile), (unsigned)cdiv(N, kWgTile),
-                                           (unsigned)chunks),
-                     dim3(kTrainThreads), 0, as_stream(stream), A, lda, M, B, ldb, N, P, chunk,
-                     amax_a, amax_b, part, bias_part);
+  const dim3 grid((unsigned)cdiv(M, kWgTile), (unsigned)cdiv(N, kWgTile), (unsigned)chunks);
+  const bool dma = P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+                   ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
+                   (int64_t)M * lda * 4 < ((int64_t)1 << 31) && (int64_t)N * ldb * 4 < ((int64_t)1 << 31);
+  if (dma) {
+    hipLaunchKernelGGL(x3_wgrad_dma_kernel, grid, dim3(kTrainThreads), 0, as_stream(stream), A,
+                       lda, M, B, ldb, N, P, amax_a, amax_b, part, bias_part);
+    return check_launch("x3_wgrad_dma_kernel");
+  }
+  hipLaunchKernelGGL(x3_wgrad_kernel, grid, dim3(kTrainThreads), 0, as_stream(stream), A, lda, M,
+                     B, ldb, N, P, chunk, amax_a, amax_b, part, bias_part);
   return check_launch("x3_wgrad_kernel");
 }
 

@@ -182,6 +182,18 @@ PARAM_NAMES = ([f"pts_linears.{i}.{k}" for i in range(8) for k in ("weight", "bi
                 "rgb_linear.weight", "rgb_linear.bias"])
 
 
+# Row padding of the feature-major activations: a row stride of P + 32 floats
+# (not P, a multiple of 2^13 at the C3 sizes) spreads the rows' same-sample
+# segments over HBM channels; measured on the weight-gradient kernel at P =
+# 196 608: 138 -> 114 us (tools/train_kernels_bench.py).
+ACT_PAD = 32
+
+
+def _act(F, P, dev):
+    """An uninitialised [F, P] activation tensor with row stride P + ACT_PAD."""
+    return torch.empty((F, P + ACT_PAD), device=dev, dtype=torch.float32)[:, :P]
+
+
 def _padded(W, cols, K):
     """[M, K] with W's columns at positions `cols` (the rest zero)."""
     out = torch.zeros((W.shape[0], K), device=W.device, dtype=torch.float32)
@@ -202,10 +214,10 @@ class NerfMLPFn(torch.autograd.Function):
         P = pts.shape[0]
         f32 = torch.float32
         enc = freq_encode(pts.detach(), XYZ_FREQS)                  # [P, 63]
-        E = torch.empty((320, P), device=dev, dtype=f32)           # cat(enc, pad, h4)
+        E = _act(320, P, dev)           # cat(enc, pad, h4)
         E[:63] = enc.t()
         E[63].zero_()                                              # h4 rows: layer 4
-        H = [torch.empty((256, P), device=dev, dtype=f32) if i not in (4,) else None
+        H = [_act(256, P, dev) if i not in (4,) else None
              for i in range(8)]
         H[4] = E[64:320]
         pk = _packs_for(params, dev)
@@ -222,7 +234,7 @@ class NerfMLPFn(torch.autograd.Function):
             src = H[i]
         h7 = H[7]
         alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
-        V = torch.empty((288, P), device=dev, dtype=f32)           # cat(feature, views enc)
+        V = _act(288, P, dev)           # cat(feature, views enc)
         V[283:].zero_()                                            # feature rows: its layer
         wf, swf, mt, nk = pk["fwd_feat"]
         _layer(wf, swf, mt, nk, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
@@ -231,7 +243,7 @@ class NerfMLPFn(torch.autograd.Function):
         amax[9:10] = _absmax(E[:63])
         amax[10:11] = _absmax(V[256:283])
         wv, swv, mt, nk = pk["fwd_views"]
-        HV = torch.empty((128, P), device=dev, dtype=f32)
+        HV = _act(128, P, dev)
         _layer(wv, swv, mt, nk, V, HV, P, bias=p["views_linears.0.bias"], relu=True)
         rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
         raw = torch.cat([rgb, alpha], 0).t().contiguous()
@@ -261,7 +273,7 @@ class NerfMLPFn(torch.autograd.Function):
         dmax = torch.zeros(10, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
         wvt, swvt, mt, nk = pk["bwd_views"]
-        DF = torch.empty((256, P), device=dev, dtype=f32)
+        DF = _act(256, P, dev)
         _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
         grads["feature_linear.weight"], grads["feature_linear.bias"] = _wgrad(
             DF, H[7], dmax[8:9], amax[7:8], with_bias=True)
@@ -269,7 +281,7 @@ class NerfMLPFn(torch.autograd.Function):
         grads["alpha_linear.bias"] = d_sig.sum(1)
         # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
         wft, swft, _, _ = pk["bwd_feat"]
-        D = torch.empty((256, P), device=dev, dtype=f32)
+        D = _act(256, P, dev)
         aw = p["alpha_linear.weight"].reshape(-1).contiguous()
         dsig = d_sig.reshape(-1).contiguous()
         _layer(wft, swft, 16, 8, DF, D, P, mask=H[7], ru=aw, rw=dsig, amax=dmax[7:8])
@@ -289,17 +301,17 @@ class NerfMLPFn(torch.autograd.Function):
             if i == 0:
                 if need_enc:
                     wt, swt, mt, nk = pk["bwd0"]
-                    de = torch.empty((64, P), device=dev, dtype=f32)
+                    de = _act(64, P, dev)
                     _layer(wt, swt, mt, nk, D, de, P)
                     d_enc = de[:63] if d_enc is None else d_enc + de[:63]
                 break
-            Dn = torch.empty((256, P), device=dev, dtype=f32)
+            Dn = _act(256, P, dev)
             if i == 5:
                 wt, swt, mt, nk = pk["bwd5h"]
                 _layer(wt, swt, mt, nk, D, Dn, P, mask=H[4], amax=dmax[i - 1:i])
                 if need_enc:
                     we, swe, mt, nk = pk["bwd5e"]
-                    de = torch.empty((64, P), device=dev, dtype=f32)
+                    de = _act(64, P, dev)
                     _layer(we, swe, mt, nk, D, de, P)
                     d_enc = de[:63]
             else:

@@ -134,6 +134,23 @@ def test_x3_wgrad_matches_matmul(dev):
         assert (got - ref).abs().max().item() / scale < 1e-6, (M, N, P)
 
 
+@pytest.mark.parametrize("M,N,P,pad", [(256, 320, 4096, 32), (3, 256, 2048, 0), (128, 288, 8192, 32),
+                                       (256, 64, 32, 32)])
+def test_x3_wgrad_dma_path(dev, M, N, P, pad):
+    """The LDS-DMA weight-gradient kernel (P % 32 == 0, aligned rows, padded row
+    strides as the training MLP allocates them): dW and the fused bias sums."""
+    from nerfhip.train_mlp import _wgrad
+    g = torch.Generator(device=dev).manual_seed(6)
+    A = torch.randn((M, P + pad), device=dev, generator=g)[:, :P]
+    B = torch.relu(torch.randn((N, P + pad), device=dev, generator=g))[:, :P]
+    got, gb = _wgrad(A, B, with_bias=True)
+    ref = A.double() @ B.double().t()
+    scale = (A.double().abs() @ B.double().abs().t()).max().item()
+    assert (got.double() - ref).abs().max().item() / scale < 1e-6
+    rb = A.double().sum(1)
+    assert (gb.double() - rb).abs().max().item() / A.double().abs().sum(1).max().item() < 1e-6
+
+
 def test_x3_packer_matches_reference_packing(dev):
     """The one-launch packer (nerf_x3_pack) == pack_x3_matrix of each padded matrix."""
     from nerfhip.train_mlp import PARAM_NAMES, X3Packer, mlp_params, pack_x3_matrix

@@ -56,6 +56,21 @@ def main():
                     f"{nbytes / ms / 1e9:7.1f} GB/s(min bytes)")
     print("\n".join(rows), flush=True)
 
+    # the weight-gradient kernel alone (no split-K sum), by row stride of A and B
+    from nerfhip import _lib
+    from nerfhip.train_mlp import wgrad_chunk
+    chunk = wgrad_chunk(P)
+    part = torch.empty((-(-P // chunk), 256, 256), device=dev)
+    for pad in (0, 32, 64, 256, 1024):
+        Ap = torch.randn((256, P + pad), device=dev, generator=g)[:, :P]
+        Bp = torch.relu(torch.randn((256, P + pad), device=dev, generator=g))[:, :P]
+        fn = lambda: _lib.call("nerf_x3_wgrad", Ap.data_ptr(), Ap.stride(0), 256, Bp.data_ptr(),
+                               Bp.stride(0), 256, P, chunk, amax.data_ptr(), amax.data_ptr(),
+                               part.data_ptr(), 0, _lib.stream_of(dev))
+        ms = timeit(fn)
+        print(f"wgrad kernel, row pad {pad:5d} floats {ms * 1e3:8.1f} us  "
+              f"{2 * 256 * P * 4 / ms / 1e9:7.2f} TB/s (A+B once)", flush=True)
+
 
 if __name__ == "__main__":
     main()
