@@ -150,7 +150,8 @@ struct Ring {
   float* base;                     // 4 x kSliceFloats
   const float4* slices;            // packed network in HBM
   int wave, lane;
-  __device__ float* buf(int g) const { return base + (g & 3) * kSliceFloats; }
+  int rot = 0;                     // ring rotation of a persistent stream (tiles x slices)
+  __device__ float* buf(int g) const { return base + ((g + rot) & 3) * kSliceFloats; }
   __device__ Dma dma_for(int g) const {   // the DMA issued while computing slice g
     const int t = g + 3;
     return make_dma(slices, t, buf(t), wave, lane);
@@ -169,11 +170,42 @@ __device__ __forceinline__ void slice_end() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Cross-lane exchange of the 4 lane groups (rows of 16 lanes) that hold one
+// sample. MLP_PERMLANE: gfx950's v_permlane16_swap / v_permlane32_swap (VALU,
+// no LDS traffic or lgkmcnt wait): swapping a value with itself leaves the
+// row pair (r0, r1) as (r0, r0) | (r1, r1), so a lane sees its xor-16 (xor-32)
+// partner in the other result. Otherwise ds_bpermute through __shfl_xor.
+#ifndef MLP_PERMLANE
+#define MLP_PERMLANE 1
+#endif
+#if MLP_PERMLANE
+// (v[l], v[l ^ 16]) in some order: both results of the swap
+__device__ __forceinline__ void pair16(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void pair32(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+#endif
+
 // sum over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48);
 // every lane of the quad ends with the bitwise-same value
+// ((v_l + v_l^16) + (v_l^32 + v_l^48) on either path: addition commutes)
 __device__ __forceinline__ float quad_sum(float v) {
+#if MLP_PERMLANE
+  float a, b;
+  pair16(v, a, b);
+  v = a + b;
+  pair32(v, a, b);
+  return a + b;
+#else
   v = v + __shfl_xor(v, 16);
   return v + __shfl_xor(v, 32);
+#endif
 }
 
 }  // namespace nerfhip

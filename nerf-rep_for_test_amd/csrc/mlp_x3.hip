@@ -142,6 +142,12 @@ constexpr int kX3DmaAhead = MLP_X3_HALF ? 2 : 3;
 #ifndef MLP_X3_LOADERS
 #define MLP_X3_LOADERS 4
 #endif
+// MLP_X3_PERSIST: one workgroup per CU loops over sample tiles; the weight
+// stream continues from one tile's last slice into the next tile's first, so
+// a tile starts on slices already resident instead of a staged prologue.
+#ifndef MLP_X3_PERSIST
+#define MLP_X3_PERSIST 1
+#endif
 #ifndef MLP_X3_LOADER_SPLIT
 #define MLP_X3_LOADER_SPLIT 0
 #endif
@@ -251,8 +257,15 @@ __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const
   load_frags<0>(fp.x, base);
 #endif
   const int t = g + kX3DmaAhead;
+#if MLP_X3_PERSIST
+  // the stream runs on into the next tile (the last tile's wrapped pieces are
+  // staged but never read): every slice stages one, every slice_end counts 2
+  const int ts = t < kX3Slices ? t : t - kX3Slices;
+#else
+  const int ts = t;
+#endif
   run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp,
-                               x3_dma(R.slices, t, R.buf(t), R.wave, R.lane), hook);
+                               x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane), hook);
 }
 
 // End of slice g: this wave's LDS-DMA of slice g+2 (XPF; g+1 without) has
@@ -293,8 +306,16 @@ struct StepViews {
 // ---------------------------------------------------------------------------
 // max over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48)
 __device__ __forceinline__ float sample_max(float v) {
+#if MLP_PERMLANE
+  float a, b;
+  pair16(v, a, b);
+  v = fmaxf(a, b);
+  pair32(v, a, b);
+  return fmaxf(a, b);
+#else
   v = fmaxf(v, __shfl_xor(v, 16));
   return fmaxf(v, __shfl_xor(v, 32));
+#endif
 }
 
 // exponent e with max * 2^e in [2^13, 2^14) (0 for an all-zero sample)
@@ -556,15 +577,33 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int g4 = lane >> 4;
-  const Ring R{ring, slices, wave, lane};
+  Ring R{ring, slices, wave, lane};
 
   for (int t = 0; t < kX3DmaAhead; ++t)
     stage_slice(make_dma(slices, t, R.buf(t), wave, lane));   // all 8 waves, 4 pieces each
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
-  const int64_t gs = (int64_t)blockIdx.x * kX3Tile + wave * 16 + (lane & 15);
+  FragPipe fp;
+  fp.late = MLP_X3_HALF ? __builtin_amdgcn_readfirstlane(wave >> 2) : 0;
+#if MLP_X3_PERSIST
+  const int64_t ntiles = (total + kX3Tile - 1) / kX3Tile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const bool first_tile = tile == (int64_t)blockIdx.x;
+#else
+  {
+  const int64_t tile = blockIdx.x;
+  constexpr bool first_tile = true;
+#endif
+  const int64_t gs = tile * kX3Tile + wave * 16 + (lane & 15);
+#if MLP_X3_PERSIST
+  // recomputed per tile: otherwise the encoding's per-lane constants are
+  // hoisted out of the tile loop and, live through every slice, spill
+  int g4 = lane >> 4;
+  asm volatile("" : "+v"(g4));
+#else
+  const int g4 = lane >> 4;
+#endif
   const bool valid = gs < total;
   const int64_t gc = valid ? gs : total - 1;
   const int64_t ray = gc / S;
@@ -582,11 +621,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 
   f32x4 acc[16];   // every layer's first slice starts it from zero
   Op X[8];
-  FragPipe fp;
-  fp.late = MLP_X3_HALF ? __builtin_amdgcn_readfirstlane(wave >> 2) : 0;
-  __syncthreads();   // head, z/rays loads and the three prologue slices resident
+  if (first_tile) __syncthreads();   // head, z/rays loads and the three prologue slices resident
 #if MLP_X3_XPF
-  load_frags<0>(fp.x, lds_base(R.buf(0), lane));   // slice 0, group 0
+  // slice 0, group 0 (a later tile's slice 0 was certified by the previous
+  // tile's slice 63; not prefetched across tiles: the fragments would stay live
+  // through the tail and the encoding)
+  load_frags<0>(fp.x, lds_base(R.buf(0), lane));
 #endif
 
   // ---- layer 0: 63 -> 256 (slices 0, 1), epilogue fused into slice 1 --------
@@ -662,12 +702,21 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     Split2 h1{{X[4], s}, {X[5], s}};
     run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>(fp);
     Split2 h2{{X[6], s}, {X[7], s}};
+#if MLP_X3_PERSIST
+    run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<2>(fp);
+    SplitHook h3{dirf, s};
+    run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<2>(fp);
+    NoHook nh;
+    const Op D[1] = {dirf};
+    run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh); x3_slice_end<2>(fp);
+#else
     run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<1>(fp);
     SplitHook h3{dirf, s};
     run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<0>(fp);
     NoHook nh;
     const Op D[1] = {dirf};
     run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh);   // the stream's last slice
+#endif
   }
   {   // views epilogue (bias, ReLU) -- once per pass, not pipelined
     const float inv = ldexpf(1.0f, -((int)hd[kHeadScales + 9] + e));
@@ -692,6 +741,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 #pragma unroll
   for (int c = 0; c < 3; ++c) rgb[c] = quad_sum(part[c]) + hd[kHeadRgbB + c];
   if (valid && g4 == 0) raw[gs] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
+  R.rot = (R.rot + kX3Slices) & 3;   // the next tile's slice 0 = this stream's slice 65
+  }
+#if MLP_X3_PERSIST
+  // the last tile's wrapped DMA pieces land before the workgroup's LDS is freed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
 
@@ -1306,7 +1361,21 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
   if (total == 0) return 0;
   const int64_t blocks = cdiv(total, kX3Tile);
   NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_forward_x3: too many samples for one launch");
-  hipLaunchKernelGGL(mlp_x3_kernel, dim3((unsigned)blocks), dim3(kX3Threads), 0,
+#if MLP_X3_PERSIST
+  // one workgroup per CU (the ring and head take 140 KiB of the 160 KiB LDS)
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+      n_cu = 256;
+  }
+  const int64_t grid = blocks < n_cu ? blocks : n_cu;
+#else
+  const int64_t grid = blocks;
+#endif
+  hipLaunchKernelGGL(mlp_x3_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
                      z_stride, total, S, (float4*)raw);
   return check_launch("mlp_x3_kernel");

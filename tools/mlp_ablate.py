@@ -48,6 +48,8 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_noenc": ["-DABL_NOENC"],
             # hook VALU interleaved into the group's MFMAs, 2 / 4 per gap
             "x3_ilv2": ["-DMLP_X3_ILV=2"], "x3_ilv4": ["-DMLP_X3_ILV=4"],
+            "x3_persist": ["-DMLP_X3_PERSIST=1"], "x3_pl": ["-DMLP_PERMLANE=1"],
+            "x3_persist_pl": ["-DMLP_X3_PERSIST=1", "-DMLP_PERMLANE=1"],
             "x3_ld4_ilv2": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_ILV=2"]}
 
 
