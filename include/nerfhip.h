@@ -109,6 +109,18 @@ int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_
 int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                   int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
                   float* part, float* bias_part, nerf_stream_t stream);
+/* nerf_freq_encode_fm: the frequency encoding of freq.py:7-32 (reference
+ *   embed_fn / embeddirs_fn, encoding/__init__.py:7-18), written feature-major
+ *   for the training MLP: out[j * ldo + p] for the 3 + 6 * n_freq columns of
+ *   torch.cat([x, sin(2^0 x), cos(2^0 x), ...], -1) of sample p (x [P][ldx],
+ *   3 coordinates). amax (nullable, device float >= 0) is raised to the
+ *   largest |out| (atomic max). */
+int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, float* out,
+                        int64_t ldo, float* amax, nerf_stream_t stream);
+/* nerf_freq_encode_fm_backward: dx [P][3] = d(encoding)/dx^T d_enc, d_enc
+ *   feature-major [3 + 6 * n_freq][ldd]. */
+int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
+                                 int64_t P, int n_freq, float* dx, nerf_stream_t stream);
 /* nerf_x3_pack: packs n weight matrices for nerf_x3_layer in one launch. descs
  * (device) = n records {const float* src; int64_t ldr, ldc; const int* rowmap;
  * const int* colmap; int M, K; void* out; int* sw} (64 bytes each): padded

@@ -499,6 +499,70 @@ __global__ void grid_update_kernel(const float* __restrict__ rays_d, const float
 
 using namespace nerfhip;
 
+// ---------------------------------------------------------------------------
+// Frequency encoding for the training MLP (freq.py:7-32), feature-major:
+// out[j][p] with j = c (raw coordinate), 3 + 6f + c (sin 2^f x_c), 6 + 6f + c
+// (cos 2^f x_c) -- the column order of torch.cat([x, sin, cos, ...], -1). One
+// thread per sample, so every output row is a coalesced store; the max |.| of
+// the block is raised into *amax (float bits as uint: all values are >= 0).
+// 2^f x is exact (power of two); sinf/cosf are the same device-library calls
+// torch's sin/cos kernels make.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void freq_encode_fm_kernel(const float* __restrict__ x,
+                                                             int64_t ldx, int64_t P, int L,
+                                                             float* __restrict__ out, int64_t ldo,
+                                                             unsigned* __restrict__ amax) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float m = 0.0f;
+  if (p < P) {
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v[c] = x[p * ldx + c];
+      out[c * ldo + p] = v[c];
+      m = fmaxf(m, fabsf(v[c]));
+    }
+    for (int f = 0; f < L; ++f) {
+      const float k = (float)(1 << f);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float a = v[c] * k;
+        const float sn = sinf(a), cs = cosf(a);
+        out[(3 + 6 * f + c) * ldo + p] = sn;
+        out[(6 + 6 * f + c) * ldo + p] = cs;
+        m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
+      }
+    }
+  }
+  if (amax) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+  }
+}
+
+// d x_c = d_enc[c] + sum_f 2^f (cos(2^f x_c) d_sin - sin(2^f x_c) d_cos): the
+// chain rule through the encoding (autograd of freq.py's cat of sin/cos).
+__global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
+    const float* __restrict__ d_enc, int64_t ldd, const float* __restrict__ x, int64_t ldx,
+    int64_t P, int L, float* __restrict__ dx) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v = x[p * ldx + c];
+    float g = d_enc[c * ldd + p];
+    for (int f = 0; f < L; ++f) {
+      const float k = (float)(1 << f);
+      const float a = v * k;
+      const float ds = d_enc[(3 + 6 * f + c) * ldd + p] * cosf(a) -
+                       d_enc[(6 + 6 * f + c) * ldd + p] * sinf(a);
+      g = g + ds * k;
+    }
+    dx[p * 3 + c] = g;
+  }
+}
+
 extern "C" {
 
 int nerf_rays(const float* cam, int H, int W, int64_t p0, int64_t n, float* rays_o,
@@ -584,6 +648,28 @@ int nerf_grid_update(const float* rays_d, const float* z, int64_t z_stride, cons
                      as_stream(stream), rays_d, z, z_stride, (const float4*)raw, weights, n, S,
                      grid, res);
   return check_launch("grid_update_kernel");
+}
+
+int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, float* out,
+                        int64_t ldo, float* amax, nerf_stream_t stream) {
+  NERF_REQUIRE(x && out, "nerf_freq_encode_fm: null pointer");
+  NERF_REQUIRE(P >= 0 && ldx >= 3 && ldo >= P && n_freq >= 0 && n_freq <= 24,
+               "nerf_freq_encode_fm: bad size");
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(freq_encode_fm_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
+                     as_stream(stream), x, ldx, P, n_freq, out, ldo, (unsigned*)amax);
+  return check_launch("freq_encode_fm_kernel");
+}
+
+int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
+                                 int64_t P, int n_freq, float* dx, nerf_stream_t stream) {
+  NERF_REQUIRE(d_enc && x && dx, "nerf_freq_encode_fm_backward: null pointer");
+  NERF_REQUIRE(P >= 0 && ldx >= 3 && ldd >= P && n_freq >= 0 && n_freq <= 24,
+               "nerf_freq_encode_fm_backward: bad size");
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(freq_encode_fm_backward_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
+                     as_stream(stream), d_enc, ldd, x, ldx, P, n_freq, dx);
+  return check_launch("freq_encode_fm_backward_kernel");
 }
 
 }  // extern "C"

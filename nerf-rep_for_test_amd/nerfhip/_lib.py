@@ -30,6 +30,8 @@ SIGNATURES = {
                            _P, _S]),
     "nerf_x3_wgrad": (_I, [_P, _I64, _I, _P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _S]),
     "nerf_x3_pack": (_I, [_P, _I, _S]),
+    "nerf_freq_encode_fm": (_I, [_P, _I64, _I64, _I, _P, _I64, _P, _S]),
+    "nerf_freq_encode_fm_backward": (_I, [_P, _I64, _P, _I64, _I64, _I, _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_sample_fine": (_I, [_P, _I64, _P, _P, _I64, _I64, _I, _I, _P, _S]),

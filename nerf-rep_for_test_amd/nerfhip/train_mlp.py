@@ -154,6 +154,13 @@ def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, r
          C.stride(0), P, ptr(amax), _lib.stream_of(C.device))
 
 
+def _encode(x, n_freq, out, amax):
+    """out[j][p] = freq_encode(x)[p][j] (x [P, 3] contiguous, out a row-strided
+    [3 + 6 n_freq, P] view); amax (a [1] device float) raised to max |out|."""
+    call("nerf_freq_encode_fm", ptr(x), 3, x.shape[0], n_freq, ptr(out), out.stride(0),
+         ptr(amax), _lib.stream_of(x.device))
+
+
 def _absmax(x):
     """max |x| as a [1] device tensor (one reduction pass)."""
     return torch.linalg.vector_norm(x, float("inf")).reshape(1)
@@ -213,18 +220,18 @@ class NerfMLPFn(torch.autograd.Function):
         dev = pts.device
         P = pts.shape[0]
         f32 = torch.float32
-        enc = freq_encode(pts.detach(), XYZ_FREQS)                  # [P, 63]
         E = _act(320, P, dev)           # cat(enc, pad, h4)
-        E[:63] = enc.t()
+        # max |.| of every saved activation (the weight-gradient scales): slots
+        # 0-7 = h0..h7 and 8 = feature from the layer kernels, 9 = xyz encoding,
+        # 10 = view encoding (both from the encoding kernel), 11 = views layer
+        amax = torch.zeros(12, device=dev, dtype=f32)
+        pts_c = pts.detach().contiguous()
+        _encode(pts_c, XYZ_FREQS, E, amax[9:10])                   # E[:63] = enc^T
         E[63].zero_()                                              # h4 rows: layer 4
         H = [_act(256, P, dev) if i not in (4,) else None
              for i in range(8)]
         H[4] = E[64:320]
         pk = _packs_for(params, dev)
-        # max |.| of every saved activation (the weight-gradient scales): slots
-        # 0-7 = h0..h7 and 8 = feature from the layer kernels, 9 = xyz encoding,
-        # 10 = view encoding
-        amax = torch.zeros(11, device=dev, dtype=f32)
         src = E[0:64]
         for i in range(8):
             wp, sw, mt, nk = pk[f"fwd{i}"]
@@ -239,15 +246,15 @@ class NerfMLPFn(torch.autograd.Function):
         wf, swf, mt, nk = pk["fwd_feat"]
         _layer(wf, swf, mt, nk, h7, V[0:256], P, bias=p["feature_linear.bias"], relu=False,
                amax=amax[8:9])
-        V[256:283] = freq_encode(dirs.detach(), DIR_FREQS).t()
-        amax[9:10] = _absmax(E[:63])
-        amax[10:11] = _absmax(V[256:283])
+        _encode(dirs.detach().contiguous(), DIR_FREQS, V[256:283], amax[10:11])
         wv, swv, mt, nk = pk["fwd_views"]
         HV = _act(128, P, dev)
-        _layer(wv, swv, mt, nk, V, HV, P, bias=p["views_linears.0.bias"], relu=True)
+        _layer(wv, swv, mt, nk, V, HV, P, bias=p["views_linears.0.bias"], relu=True,
+               amax=amax[11:12])
         rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
         raw = torch.cat([rgb, alpha], 0).t().contiguous()
-        ctx.save_for_backward(pts, E, *H[:4], *H[5:], V, HV, amax, *params)
+        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, *params)
+        ctx.pts_grad = pts.requires_grad
         ctx.packs = pk
         return raw
 
@@ -263,7 +270,7 @@ class NerfMLPFn(torch.autograd.Function):
         grads = {}
         d_raw = d_raw.t().contiguous()                              # [4, P]
         d_rgb, d_sig = d_raw[0:3], d_raw[3:4]
-        grads["rgb_linear.weight"] = _wgrad(d_rgb, HV)            # K = P: x3 split-K GEMM
+        grads["rgb_linear.weight"] = _wgrad(d_rgb, HV, amax_b=amax[11:12])   # K = P: x3 split-K
         grads["rgb_linear.bias"] = d_rgb.sum(1)
         d_hv = (p["rgb_linear.weight"].t() @ d_rgb) * (HV > 0)      # [128, P]
         wv = p["views_linears.0.weight"]                            # [128, 283]
@@ -297,7 +304,7 @@ class NerfMLPFn(torch.autograd.Function):
                 gw = torch.cat([gw[:, :63], gw[:, 64:320]], 1)
             grads[f"pts_linears.{i}.weight"] = gw
             grads[f"pts_linears.{i}.bias"] = gb
-            need_enc = pts.requires_grad and ctx.needs_input_grad[0]
+            need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
             if i == 0:
                 if need_enc:
                     wt, swt, mt, nk = pk["bwd0"]
@@ -320,10 +327,9 @@ class NerfMLPFn(torch.autograd.Function):
             D = Dn
         d_pts = None
         if d_enc is not None:
-            with torch.enable_grad():
-                x = pts.detach().requires_grad_(True)
-                enc = freq_encode(x, XYZ_FREQS)
-                (d_pts,) = torch.autograd.grad(enc, x, d_enc.t())
+            d_pts = torch.empty((P, 3), device=dev, dtype=f32)
+            call("nerf_freq_encode_fm_backward", ptr(d_enc), d_enc.stride(0), ptr(pts), 3, P,
+                 XYZ_FREQS, ptr(d_pts), _lib.stream_of(dev))
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
 
 
