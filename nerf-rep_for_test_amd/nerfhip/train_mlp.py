@@ -15,8 +15,10 @@ DESIGN.md §3), in both directions:
   dgrad     d_{L-1} = (W_L^T d_L) * (h_{L-1} > 0)
   wgrad     dW_L = d_L h_{L-1}^T  (``nerf_x3_wgrad``, split-K partials summed)
 
-The rank-1 heads (alpha 256->1, rgb 128->3), bias gradients (row sums) and
-the frequency encoding with its derivative are small torch ops on the device.
+The frequency encoding and its derivative are HIP kernels that write / read
+the feature-major rows directly (``nerf_freq_encode_fm`` / ``_backward``, the
+encoding's max |.| fused); the rank-1 heads (alpha 256->1, rgb 128->3) and
+the bias gradients (row sums) are small torch ops on the device.
 Weights are repacked from the live parameters every call (device-side torch
 ops, no host sync): packing order = ``pack_x3_matrix``.
 """
