@@ -66,3 +66,73 @@ def rel_err(a, b, floor=1.0):
 def psnr(a, b):
     mse = float(np.mean((np.clip(a, 0, 1).astype(np.float64) - np.clip(b, 0, 1)) ** 2))
     return float("inf") if mse == 0 else -10.0 * np.log10(mse)
+
+
+# --------------------------------------------------------------------------
+# End-to-end fine-map gate against the reference's own float32 noise floor.
+#
+# tests/golden/s_<fixture>.npz (make_sensitivity.py) holds, per ray, the largest
+# deviation of the reference from its own golden render over 16 exact
+# reparametrisations of the network (hidden units permuted: same function,
+# another GEMM summation order; half of them also with a +-1-ulp libm). The
+# reference itself keeps only 46-85 % of rays within 1e-5 on the fine maps of
+# the C2-type synthetic fixtures (VR:239-268 is
+# ill-conditioned in the coarse weights' rounding), so a fixed 1e-5 on every
+# ray is not a property any float32 implementation has. The gate instead holds
+# an implementation to that floor ray by ray:
+#   (1) >= 99 % of rays: |err| <= 4 x max(tol, reference spread) on every map
+#   (2) fraction of rays within tol >= the worst reparametrised reference - 0.02
+#   (3) fine rgb PSNR vs golden >= min(80 dB, median reparametrised PSNR - 6 dB)
+# where tol = 1e-5 abs (rgb, acc), 1e-5 x max(1, |depth|) (depth) and
+# 1e-4 x max(1e-3, |disp|) (disp); a NaN-pattern change is an infinite error
+# unless the reference itself flipped NaN on that ray.
+# --------------------------------------------------------------------------
+FINE_KEYS = ("rgb_map", "acc_map", "depth_map", "disp_map")
+GATE_RATIO = 4.0
+GATE_FRAC = 0.99
+
+
+def _tol(key, ref):
+    if key.startswith("depth"):
+        return 1e-5 * np.maximum(1.0, np.abs(ref))
+    if key.startswith("disp"):
+        return 1e-4 * np.maximum(1e-3, np.abs(np.nan_to_num(ref)))
+    return np.full(ref.shape, 1e-5)
+
+
+def ray_errors(res, z, n, keys=FINE_KEYS):
+    """key -> (per-ray max abs error, per-ray tolerance) against the golden maps."""
+    out = {}
+    for k in keys:
+        a = np.asarray(res[k], np.float64).reshape(n, -1)
+        b = np.asarray(z["out_" + k], np.float64).reshape(n, -1)
+        e = np.nan_to_num(np.abs(a - b), nan=0.0).max(-1)
+        e[(np.isnan(a) != np.isnan(b)).any(-1)] = np.inf
+        tol = _tol(k, np.nan_to_num(b, nan=0.0)).max(-1)
+        out[k] = (e, tol)
+    return out
+
+
+def fine_gate(res, z, s):
+    """Evaluate the three criteria above; returns (ok, report dict)."""
+    n = int(z["H"]) * int(z["W"])
+    errs = ray_errors(res, z, n)
+    ratio = np.zeros(n)
+    within = np.ones(n, bool)
+    for k, (e, tol) in errs.items():
+        sp = s["spread_" + k].astype(np.float64)
+        r = np.where(np.isinf(sp), 0.0, e / np.maximum(sp, tol))
+        ratio = np.maximum(ratio, r)
+        if k != "disp_map":
+            within &= e <= tol
+    p = psnr(np.reshape(res["rgb_map"], (n, 3)), np.reshape(z["out_rgb_map"], (n, 3)))
+    vp = np.asarray(s["variant_psnr"], np.float64)
+    rep = {"frac_ratio_ok": float(np.mean(ratio <= GATE_RATIO)),
+           "frac_within_tol": float(within.mean()),
+           "ref_self_frac_within_tol_min": float(np.min(s["variant_frac_ok"])),
+           "psnr": p, "ref_self_psnr_median": float(np.median(vp)),
+           "worst_ratio": float(ratio.max()), "n": n}
+    ok = (rep["frac_ratio_ok"] >= GATE_FRAC
+          and rep["frac_within_tol"] >= rep["ref_self_frac_within_tol_min"] - 0.02
+          and p >= min(80.0, rep["ref_self_psnr_median"] - 6.0))
+    return ok, rep

@@ -3,14 +3,16 @@
 Stage tests feed the HIP kernel and the oracle identical inputs; end-to-end
 tests render the golden fixtures' cameras. Tolerances (north_star): rgb/acc
 within 1e-5 abs, depth within 1e-5 relative to its magnitude, disp NaN-aware.
-Fine maps end-to-end are checked by PSNR (fine depths depend on float32 MLP
-rounding) and exactly-staged by feeding reference depths.
+Fine maps end-to-end are held ray by ray to the reference's own float32 noise
+floor (goldlib.fine_gate, tests/golden/make_sensitivity.py: the reference itself
+keeps only 46-85 % of rays within 1e-5 under an exact reparametrisation of its
+network), and exactly-staged by feeding the reference's own depths.
 """
 import numpy as np
 import pytest
 
 from conftest import golden_names
-from goldlib import grid_of, load, max_err, oracle_cfg, params_of, psnr, rel_err
+from goldlib import MAP_KEYS, fine_gate, grid_of, load, max_err, oracle_cfg, params_of, psnr, rel_err
 from oracle import nerf_oracle as O
 
 torch = pytest.importorskip("torch")
@@ -288,11 +290,14 @@ def test_render_coarse_maps_vs_golden(dev, name, prec):
 
 @pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5")])
 @pytest.mark.parametrize("prec", ["fp32", "f16x3"])
-def test_render_fine_maps_psnr_vs_golden(dev, name, prec):
+def test_render_fine_maps_per_ray_gate(dev, name, prec):
+    """All four fine maps end to end, ray by ray: >= 99 % of rays within 4x the
+    reference's own reparametrisation spread (or 1e-5), the fraction within 1e-5
+    no worse than the reparametrised reference's, PSNR >= min(80, its median - 6)."""
     z = load(name)
     _, res = _render_fixture(dev, z, prec)
-    n = int(z["H"]) * int(z["W"])
-    assert psnr(res["rgb_map"], z["out_rgb_map"].reshape(n, 3)) > 35.0
+    ok, rep = fine_gate(res, z, load("s_" + name))
+    assert ok, rep
 
 
 @pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5") and "ert" not in n])
@@ -340,7 +345,13 @@ def test_renderer_plugin_contract(dev):
                         "rgb_map", "disp_map", "acc_map", "depth_map"}
     assert out["rgb_map"].shape == (32, 32, 3) and out["acc_map"].shape == (32, 32)
     assert out["rgb_map"].device.type == "cuda"
-    assert max_err(out["rgb_map_0"].cpu().numpy(), z["out_rgb_map_0"]) < TOL
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    assert max_err(got["rgb_map_0"], z["out_rgb_map_0"]) < TOL
+    assert max_err(got["acc_map_0"], z["out_acc_map_0"]) < TOL
+    assert rel_err(got["depth_map_0"], z["out_depth_map_0"]) < TOL
+    assert rel_err(got["disp_map_0"], z["out_disp_map_0"], floor=1e-3) < 1e-4
+    ok, rep = fine_gate(got, z, load("s_f1_c2_crop"))
+    assert ok, rep
     reset()
 
 
