@@ -318,12 +318,17 @@ __device__ __forceinline__ float sample_max(float v) {
 #endif
 }
 
-// exponent e with max * 2^e in [2^13, 2^14) (0 for an all-zero sample)
+// exponent e with max * 2^e in [2^13, 2^14) (0 for an all-zero sample), at
+// most kMaxActExp: a sample whose values are all below 2^-50 (training: the
+// gradient of a sample far behind an opaque surface underflows towards the
+// FP32 denormals) would otherwise get 2^e = inf and 0 * inf = NaN; capped, its
+// splits flush to 0, below the FP32 rounding of any sum it enters.
+constexpr int kMaxActExp = 64;
 __device__ __forceinline__ int act_exponent(float mx) {
   if (!(mx > 0.0f)) return 0;
   int E;
   (void)frexpf(mx, &E);   // mx in [2^(E-1), 2^E)
-  return 14 - E;
+  return min(14 - E, kMaxActExp);
 }
 
 // FP16 hi/lo of two scaled values, packed: (hi pair, lo pair) as two dwords

@@ -37,6 +37,31 @@ def load_gt(path, H=None, W=None):
     return resize_bilinear(img, H or img.shape[0], W or img.shape[1])
 
 
+def decode_png(buf):
+    """uint8 PNG file bytes -> float32 [H,W,C] in [0, 1] (blender.py:53-56: /255)."""
+    import io
+    from PIL import Image
+    return np.asarray(Image.open(io.BytesIO(np.asarray(buf).tobytes())), np.float32) / \
+        np.float32(255.0)
+
+
+def load_packed(path, H=None, W=None, indices=None):
+    """Views packed by tools/pack_lego.py as the reference's dataset yields them
+    (blender.py:38-84): white-composited RGB [N,H,W,3] float32, poses [N,4,4],
+    focal (0.5 W / tan(0.5 camera_angle_x), blender.py:41-42) and the json frame
+    indices."""
+    z = np.load(path)
+    offs = z["png_offsets"]
+    idx = range(len(offs) - 1) if indices is None else indices
+    imgs = []
+    for i in idx:
+        img = composite_white(decode_png(z["png_bytes"][offs[i]:offs[i + 1]]))
+        imgs.append(resize_bilinear(img, H or img.shape[0], W or img.shape[1]))
+    imgs = np.stack(imgs)
+    focal = 0.5 * imgs.shape[2] / np.tan(0.5 * float(z["camera_angle_x"]))
+    return imgs, z["poses"][list(idx)], float(focal), z["frames"][list(idx)]
+
+
 def psnr(pred, gt):
     pred = np.clip(np.asarray(pred, np.float64), 0, 1)
     gt = np.clip(np.asarray(gt, np.float64), 0, 1)

@@ -200,3 +200,28 @@ def test_freq_encode_fm_matches_torch(dev, P, L):
     xr = x.clone().requires_grad_(True)
     (gr,) = torch.autograd.grad(freq_encode(xr, L), xr, d_enc.t())
     assert _rel(dx, gr) < 1e-5
+
+
+def test_x3_train_mlp_denormal_sample_gradients(dev):
+    """Samples whose output gradient underflows (rays behind an opaque surface:
+    transmittance ~ 0, d raw ~ 1e-40) must not turn the per-sample FP16 split
+    scale into inf (0 * inf = NaN in every parameter gradient); they contribute
+    nothing, as in FP32."""
+    from nerfhip.train import freq_encode
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    m = _model(dev)
+    P = 2048
+    pts, dirs = _inputs(dev, P, seed=4)
+    g = torch.Generator(device=dev).manual_seed(5)
+    d_raw = torch.randn((P, 4), device=dev, generator=g)
+    d_raw[P // 2:] *= 1e-40                       # FP32 denormals
+    d_raw[P // 4:P // 2] = 0.0
+    x = pts.clone().requires_grad_(True)
+    ref = m(torch.cat([freq_encode(x, 10), freq_encode(dirs, 4)], -1))
+    ref_grads = torch.autograd.grad(ref, [x] + mlp_params(m), d_raw)
+    y = pts.clone().requires_grad_(True)
+    out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+    got = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
+    for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads):
+        assert torch.isfinite(a).all(), name
+        assert _rel(a, b) < 1e-4, (name, _rel(a, b))
