@@ -82,12 +82,16 @@ def sample_pdf(mids, weights, u):
     return bin_lo + t * (bin_hi - bin_lo)
 
 
-def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query):
+def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query,
+                 detach_fine_samples=False):
     """The differentiable part of a training step (VR:164-194): coarse depths z
     [n, S] (no gradient) -> coarse maps, importance samples from the coarse
     weights (u [n, N_importance]), fine maps. fine=None: coarse only.
     query_fn(model, pts, dirs) evaluates the MLP (torch module call, or the x3
-    MFMA kernels of train_mlp.query_x3)."""
+    MFMA kernels of train_mlp.query_x3). The reference lets the fine loss's
+    gradient flow through the importance samples into the coarse network (no
+    detach, VR:181-184, 239-268); detach_fine_samples=True stops it there, as
+    the original NeRF does (tf.stop_gradient on z_samples)."""
     pts = rays_o[:, None, :] + rays_d[:, None, :] * z[..., None]
     raw = query_fn(coarse, pts, rays_d)
     rgb0, disp0, acc0, w, depth0 = composite(raw, z, rays_d, white_bkgd)
@@ -95,6 +99,8 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
     if fine is not None:
         mids = 0.5 * (z[..., 1:] + z[..., :-1])
         zf = sample_pdf(mids, w[..., 1:-1], u)
+        if detach_fine_samples:
+            zf = zf.detach()
         z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
         pts2 = rays_o[:, None, :] + rays_d[:, None, :] * z2[..., None]
         raw2 = query_fn(fine, pts2, rays_d)
@@ -117,7 +123,8 @@ class NerfTrainer:
     """Coarse + fine networks, optimizer and one training step on a ROCm device."""
 
     def __init__(self, device, params, N_samples=64, N_importance=128, near=2.0, far=6.0,
-                 white_bkgd=True, lr=5e-4, clip_value=40.0, mlp="x3"):
+                 white_bkgd=True, lr=5e-4, clip_value=40.0, mlp="x3",
+                 detach_fine_samples=False):
         from src.models.nerf.network import NeRF
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -129,6 +136,7 @@ class NerfTrainer:
         if mlp not in ("x3", "torch"):
             raise ValueError("mlp must be 'x3' or 'torch'")
         self.mlp = mlp
+        self.detach_fine_samples = bool(detach_fine_samples)
         self.coarse = NeRF().to(self.device)
         self.fine = NeRF().to(self.device)
         self.load(params)
@@ -162,7 +170,7 @@ class NerfTrainer:
         from .train_mlp import query_x3
         return render_train(self.coarse, self.fine if self.N_importance > 0 else None,
                             rays_o, rays_d, z, u, self.white_bkgd,
-                            query_x3 if self.mlp == "x3" else query)
+                            query_x3 if self.mlp == "x3" else query, self.detach_fine_samples)
 
     def loss(self, out, target):
         return mse_losses(out, target)

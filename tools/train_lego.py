@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--ckpt-every", type=int, default=5000)
     ap.add_argument("--eval-frames", type=int, default=25)
     ap.add_argument("--mlp", default="x3", choices=["x3", "torch"])
+    ap.add_argument("--detach-fine-samples", action="store_true",
+                    help="stop the fine loss's gradient at the importance samples (original "
+                         "NeRF); the reference lets it reach the coarse network")
     ap.add_argument("--check-finite", action="store_true",
                     help="stop at the first step whose loss or parameters are not finite")
     args = ap.parse_args()
@@ -86,7 +89,7 @@ def main():
     for prefix in ("model", "model_fine"):          # nn.Linear default initialisation
         for k, v in NeRF().state_dict().items():
             init[f"{prefix}.{k}"] = v
-    tr = NerfTrainer(dev, init, mlp=args.mlp)
+    tr = NerfTrainer(dev, init, mlp=args.mlp, detach_fine_samples=args.detach_fine_samples)
     step0 = 0
     if args.resume:
         ck = load_checkpoint(args.resume)
@@ -137,7 +140,7 @@ def main():
                       flush=True)
                 break
         if step % args.log_every == 0:
-            lc, lf = float(losses["loss_coarse"]), float(losses["loss_fine"])
+            lc, lf = float(losses["loss_coarse"].detach()), float(losses["loss_fine"].detach())
             now = time.perf_counter()
             rec = {"step": step, "loss": lc + lf, "psnr_coarse": -10 * math.log10(lc),
                    "psnr_fine": -10 * math.log10(lf), "lr": args.lr * math.exp(gamma * step),
