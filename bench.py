@@ -128,7 +128,7 @@ def main():
         def frame(i):
             pose, K = lego_camera(H, W, i)
             return render_frame_sharded(
-                lambda p0, n: pipe.render_image(H, W, pose, K, p0=p0, n=n),
+                lambda p0, n: pipe.render_band(H, W, pose, K, p0, n),
                 H, W, rank, world, dev, chunk_aligned=c4)
 
         for i in range(args.warmup):

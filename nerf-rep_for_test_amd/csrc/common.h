@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
 #include <string>
 
 #include "../../include/nerfhip.h"
@@ -23,6 +25,27 @@ int check_launch(const char* what);
   } while (0)
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// CU count of the device a stream launches on (persistent grids: one workgroup
+// per CU), cached per device ordinal; races only write the same value. The
+// null/legacy stream resolves to the calling thread's current device.
+inline int stream_cu_count(nerf_stream_t s) {
+  static std::atomic<int> cache[64];
+  hipDevice_t dev = 0;
+  if (hipStreamGetDevice(as_stream(s), &dev) != hipSuccess) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return 256;
+    dev = cur;
+  }
+  if (dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      n <= 0)
+    return 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
 
 // ---------------------------------------------------------------------------
 // torch CPU float32 reductions (ATen SumKernel, x86 build): bit-exact orders.

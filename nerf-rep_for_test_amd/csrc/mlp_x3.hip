@@ -1368,14 +1368,7 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
   NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_forward_x3: too many samples for one launch");
 #if MLP_X3_PERSIST
   // one workgroup per CU (the ring and head take 140 KiB of the 160 KiB LDS)
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n_cu <= 0)
-      n_cu = 256;
-  }
+  const int n_cu = stream_cu_count(stream);
   const int64_t grid = blocks < n_cu ? blocks : n_cu;
 #else
   const int64_t grid = blocks;
@@ -1391,9 +1384,10 @@ static int launch_layer(const float* w, const int* sw, const float* bias, const 
                         int64_t ldb, const float* mask, int64_t ldm, const float* ru,
                         const float* rw, float* C, int64_t ldc, int64_t P, float* amax_out,
                         nerf_stream_t stream) {
-  // persistent: at most 256 workgroups (one per CU: the ring takes 64-128 KiB of LDS)
+  // persistent: at most one workgroup per CU (the ring takes 64-128 KiB of LDS)
   const int64_t tiles = cdiv(P, kTrainTile);
-  hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)(tiles < 256 ? tiles : 256)),
+  const int n_cu = stream_cu_count(stream);
+  hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)(tiles < n_cu ? tiles : n_cu)),
                      dim3(kTrainThreads), 0, as_stream(stream), (const uint4*)w, sw, bias, B,
                      ldb, mask, ldm, ru, rw, C, ldc, P, amax_out);
   return check_launch("x3_layer_kernel");

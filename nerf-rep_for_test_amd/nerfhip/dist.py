@@ -6,7 +6,10 @@ independent with ESS/ERT off, so rank r renders pixel rows
 [r*H/P, (r+1)*H/P) and the 12 float32 maps per pixel (rgb_0, disp_0, acc_0,
 depth_0, rgb, disp, acc, depth) are all-gathered as equal-size tiles. With
 ERT/ESS on, chunk membership (2048 consecutive pixels) changes results, so
-bands are cut on whole reference chunks instead (``chunk_aligned=True``).
+bands are cut on whole reference chunks instead (``chunk_aligned=True``), and
+with ESS + ERT each rank replays the grid self-updates of the chunks outside
+its band (NerfPipeline.render_band) so that every band sees the grid the
+reference's sequential loop would have at its first chunk.
 """
 from __future__ import annotations
 
@@ -59,11 +62,13 @@ def unpack_maps(full, H, W, keys):
 
 def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
                          chunk_aligned=False):
-    """render_band(p0, n) -> dict of flat maps for pixels [p0, p0+n).
+    """render_band(p0, n) -> dict of flat maps for pixels [p0, p0+n) ({} when n
+    is 0; it is called on every rank, so stateful renderers -- ESS + ERT,
+    NerfPipeline.render_band -- advance their grid and counter everywhere).
 
     Returns the assembled frame (dict of [H,W(,3)] maps) on every rank."""
     p0, n, n_pad = band(H, W, rank, world, chunk_aligned)
-    maps = render_band(p0, n) if n > 0 else {}
+    maps = render_band(p0, n) or {}
     keys = set(maps) if maps else set(MAP_ORDER)
     tile = pack_maps(maps, n, n_pad, device)
     if world == 1:

@@ -242,6 +242,50 @@ class NerfPipeline:
              _lib.stream_of(self.device))
         return rays_o, rays_d
 
+    def render_band(self, H, W, pose, K, p0, n):
+        """Pixels [p0, p0+n) of a frame whose other pixels other ranks render
+        concurrently, with the results of the reference's sequential chunk loop
+        (VR:147-205). Without ESS+ERT that is render_image. With both, the ESS
+        grid self-updates at the chunks whose ERT call counter hits a multiple of
+        grid_update_interval (VR:1147-1157) and later chunks sample against the
+        updated grid (VR:1009-1087), so a band must see every earlier update:
+        this rank replays each updating chunk before its band (in chunk order,
+        each replay at that chunk's counter), renders its band at the counter of
+        its first chunk, then replays the updating chunks after its band, so
+        that every rank leaves the frame with the grid and counter the
+        sequential loop ends with. Bands start on 2048-ray chunk boundaries.
+        Cost: one extra chunk per update outside the band (2 per 500 calls).
+        Returns the map dict ({} for an empty band)."""
+        per = self._calls_per_chunk()
+        cf = self.grid_update_counter
+        total = -(-H * W // REF_CHUNK)
+        if not (self.enable_ess and self.enable_ert):
+            res = self.render_image(H, W, pose, K, p0=p0, n=n) if n > 0 else {}
+            if self.enable_ert:       # the counter only drives ESS grid updates
+                self.grid_update_counter = cf + per * total
+            return res
+        if p0 % REF_CHUNK:
+            raise ValueError("with ESS + ERT a band must start on a 2048-ray chunk boundary")
+        c0, c1 = p0 // REF_CHUNK, -(-(p0 + n) // REF_CHUNK)
+        upd = [c for c in range(total)
+               if any((cf + per * c + k) % self.grid_update_interval == 0 for k in range(per))]
+
+        def replay(c):
+            self.grid_update_counter = cf + per * c
+            a = c * REF_CHUNK
+            self.render_image(H, W, pose, K, p0=a, n=min(REF_CHUNK, H * W - a))
+
+        for c in upd:
+            if c < c0:
+                replay(c)
+        self.grid_update_counter = cf + per * c0
+        res = self.render_image(H, W, pose, K, p0=p0, n=n) if n > 0 else {}
+        for c in upd:
+            if c >= c1:
+                replay(c)
+        self.grid_update_counter = cf + per * total
+        return res
+
     def render_image(self, H, W, pose, K, t_rand=None, u=None, p0=0, n=None):
         """Render pixels [p0, p0+n) of an H x W image; returns the reference's map dict
         (``rgb_map_0, disp_map_0, acc_map_0, depth_map_0`` + fine maps), flat per pixel."""

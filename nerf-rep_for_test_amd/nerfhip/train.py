@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import call, ptr
-from .render import coarse_depth_table
+from .render import REF_CHUNK, coarse_depth_table
 
 XYZ_FREQS, DIR_FREQS = 10, 4
 
@@ -82,8 +82,41 @@ def sample_pdf(mids, weights, u):
     return bin_lo + t * (bin_hi - bin_lo)
 
 
+def composite_ert(raw, z, rays_d, thr, white_bkgd, chunk=2048):
+    """VR:1089-1133 (raw_noise_std = 0), differentiable: transmittance WITHOUT the
+    +1e-10; where any ray of a 2048-ray chunk has T < thr, every ray of that
+    chunk has its weights zeroed from its first such sample on (argmax of an
+    all-False row is 0: a ray that never terminates loses all of its weights,
+    quirk 1). Rows [0, n) start on a chunk boundary of the reference's loop."""
+    n, S = z.shape
+    ones = torch.full_like(z[..., :1], 1e10)
+    dists = torch.cat([z[..., 1:] - z[..., :-1], ones], -1)
+    dists = dists * torch.norm(rays_d[..., None, :], dim=-1)
+    rgb = torch.sigmoid(raw[..., :3])
+    alpha = 1.0 - torch.exp(-F.relu(raw[..., 3]) * dists)
+    shifted = torch.cat([torch.zeros_like(alpha[:, :1]), alpha[:, :-1]], 1)
+    trans = torch.cumprod(1.0 - shifted, 1)
+    w = alpha * trans
+    low = trans < thr
+    nc = -(-n // chunk)
+    ray_any = low.any(1)
+    pad = torch.zeros(nc * chunk - n, dtype=torch.bool, device=z.device)
+    chunk_any = torch.cat([ray_any, pad]).view(nc, chunk).any(1)
+    cut = chunk_any.repeat_interleave(chunk)[:n]
+    first = low.float().argmax(1)
+    mask = (torch.arange(S, device=z.device)[None, :] >= first[:, None]) & cut[:, None]
+    w = w * (~mask).float()
+    rgb_map = torch.sum(w[..., None] * rgb, -2)
+    depth = torch.sum(w * z, -1)
+    acc = torch.sum(w, -1)
+    disp = 1.0 / torch.max(torch.full_like(depth, 1e-10), depth / torch.sum(w, -1))
+    if white_bkgd:
+        rgb_map = rgb_map + (1.0 - acc[..., None])
+    return rgb_map, disp, acc, w, depth
+
+
 def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query,
-                 detach_fine_samples=False):
+                 detach_fine_samples=False, composite_fn=None, on_composite=None):
     """The differentiable part of a training step (VR:164-194): coarse depths z
     [n, S] (no gradient) -> coarse maps, importance samples from the coarse
     weights (u [n, N_importance]), fine maps. fine=None: coarse only.
@@ -91,10 +124,18 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
     MFMA kernels of train_mlp.query_x3). The reference lets the fine loss's
     gradient flow through the importance samples into the coarse network (no
     detach, VR:181-184, 239-268); detach_fine_samples=True stops it there, as
-    the original NeRF does (tf.stop_gradient on z_samples)."""
+    the original NeRF does (tf.stop_gradient on z_samples).
+    composite_fn(raw, z, rays_d) -> (rgb, disp, acc, weights, depth) replaces
+    _raw2outputs (e.g. composite_ert); on_composite(kind, z, raw, weights) is
+    called after each composite (kind 0 coarse, 1 fine: the ESS grid hook)."""
+    if composite_fn is None:
+        def composite_fn(raw, zz, rd):
+            return composite(raw, zz, rd, white_bkgd)
     pts = rays_o[:, None, :] + rays_d[:, None, :] * z[..., None]
     raw = query_fn(coarse, pts, rays_d)
-    rgb0, disp0, acc0, w, depth0 = composite(raw, z, rays_d, white_bkgd)
+    rgb0, disp0, acc0, w, depth0 = composite_fn(raw, z, rays_d)
+    if on_composite is not None:
+        on_composite(0, z, raw, w)
     out = {"rgb_map_0": rgb0, "disp_map_0": disp0, "acc_map_0": acc0, "depth_map_0": depth0}
     if fine is not None:
         mids = 0.5 * (z[..., 1:] + z[..., :-1])
@@ -104,9 +145,76 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
         z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
         pts2 = rays_o[:, None, :] + rays_d[:, None, :] * z2[..., None]
         raw2 = query_fn(fine, pts2, rays_d)
-        rgb, disp, acc, _, depth = composite(raw2, z2, rays_d, white_bkgd)
+        rgb, disp, acc, w2, depth = composite_fn(raw2, z2, rays_d)
+        if on_composite is not None:
+            on_composite(1, z2, raw2, w2)
         out.update(rgb_map=rgb, disp_map=disp, acc_map=acc, depth_map=depth)
     return out
+
+
+def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
+                      detach_fine_samples=False):
+    """The reference's training-mode ``_render_pytorch`` over a ray block
+    (VR:145-216 with ``self.net.training``): per 2048-ray chunk, in the
+    reference's order, the perturb draw t_rand [m, S] (VR:228-235 / ESS
+    :1080-1085) then the fine draw u [m, N_importance] (VR:247-249), both
+    torch.rand on the device; coarse depths by the HIP kernels (stratified or
+    ESS, no gradient); MLPs + compositing differentiable (render_train), ERT
+    with its chunk rule (composite_ert), the ESS grid self-update and call
+    counter of VR:1147-1157 on detached values, passes cut after a
+    grid-updating chunk as in NerfPipeline.render_rays. ``pipe`` is the
+    NerfPipeline holding the configuration, tables, grid and counter."""
+    n = rays_o.shape[0]
+    S, NI = pipe.N_samples, pipe.N_importance
+    dev = pipe.device
+    st = _lib.stream_of(dev)
+    outs = []
+    p = 0
+    while p < n:
+        m = n - p
+        if pipe.enable_ess and pipe.enable_ert:
+            m = pipe._ess_phase_len(m)
+        ro, rd = rays_o[p:p + m], rays_d[p:p + m]
+        tr, uu = [], []
+        for c0 in range(0, m, REF_CHUNK):
+            mc = min(REF_CHUNK, m - c0)
+            if perturb > 0:
+                tr.append(torch.rand((mc, S), device=dev))
+            if NI > 0:
+                uu.append(torch.rand((mc, NI), device=dev))
+        t_rand = torch.cat(tr).contiguous() if tr else None
+        u = torch.cat(uu).contiguous() if uu else None
+        z = torch.empty((m, S), device=dev, dtype=torch.float32)
+        if pipe.enable_ess:
+            if pipe.grid is None:
+                raise _lib.NerfHipError("ESS enabled but no occupancy grid set")
+            call("nerf_sample_coarse_ess", ptr(ro), ptr(rd), ptr(pipe.grid), pipe.grid_res,
+                 ptr(pipe.z_base), ptr(t_rand), m, S, REF_CHUNK, pipe.ess_skip_threshold,
+                 ptr(z), st)
+        elif t_rand is not None:
+            call("nerf_sample_coarse", ptr(pipe.z_base), ptr(t_rand), m, S, ptr(z), st)
+        else:
+            z.copy_(pipe.z_base.expand(m, S))
+        counter0 = pipe.grid_update_counter
+        comp, hook = None, None
+        if pipe.enable_ert:
+            def comp(raw, zz, rdd):
+                return composite_ert(raw, zz, rdd, pipe.ert_threshold, pipe.white_bkgd)
+
+            def hook(kind, zz, raw, w):
+                ss = zz.shape[1]
+                pipe._grid_updates(kind, counter0, rd, zz.detach().contiguous(), ss,
+                                   raw.detach().reshape(-1, 4).contiguous(),
+                                   w.detach().contiguous(), m, ss)
+        else:
+            def comp(raw, zz, rdd):
+                return composite(raw, zz, rdd, pipe.white_bkgd)
+        outs.append(render_train(coarse, fine if NI > 0 else None, ro, rd, z, u,
+                                 pipe.white_bkgd, query_fn, detach_fine_samples, comp, hook))
+        if pipe.enable_ert:
+            pipe.grid_update_counter = counter0 + pipe._calls_per_chunk() * -(-m // REF_CHUNK)
+        p += m
+    return {k: torch.cat([o[k] for o in outs], 0) for k in outs[0]}
 
 
 def mse_losses(out, target):
@@ -187,16 +295,20 @@ class NerfTrainer:
         self.opt.zero_grad(set_to_none=True)
         losses = self.loss(self.forward(rays_o, rays_d, t_rand, u), target)
         losses["loss"].backward()
-        if group is not None:
-            allreduce_mean([p.grad for p in self.parameters()], group)
+        if group is not None:   # parameters without a gradient (e.g. no fine pass) skipped
+            allreduce_mean([p.grad for p in self.parameters() if p.grad is not None], group)
         torch.nn.utils.clip_grad_value_(self.parameters(), self.clip_value)
         self.opt.step()
         return losses
 
 
 def allreduce_mean(grads, group):
-    """Average gradients over the group in one flat bucket (2.4 MB per network)."""
+    """Average gradients over the group in one flat bucket (2.4 MB per network).
+    None entries are skipped (every rank has the same set: same configuration)."""
     import torch.distributed as dist
+    grads = [g for g in grads if g is not None]
+    if not grads:
+        return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, group=group)
     flat /= dist.get_world_size(group)

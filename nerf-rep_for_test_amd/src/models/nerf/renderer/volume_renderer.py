@@ -50,6 +50,7 @@ class Renderer:
         self.cuda_threads = getattr(cfg, "cuda_threads", 256)
         if not self.use_viewdirs:
             raise NotImplementedError("use_viewdirs=False is not on the lego render path")
+        self._check_topology()
         if self.raw_noise_std and float(self.raw_noise_std) > 0:
             raise NotImplementedError("raw_noise_std > 0 (training-time density noise) "
                                       "is not implemented in the HIP path")
@@ -68,13 +69,42 @@ class Renderer:
         if self.enable_ess:
             self._initialize_occupancy_grid()
 
+    def _check_topology(self):
+        """The HIP kernels implement exactly the lego network (lego.yaml:29-44):
+        xyz / dir frequency encodings with L = 10 / 4 (63 / 27 inputs), 8 x 256
+        layers with the skip after layer 4, a 128-wide views layer. Anything else
+        is refused here rather than packed wrongly."""
+        from nerfhip.synthetic import layer_shapes
+        net_cfg = cfg.get("network", {}) if hasattr(cfg, "get") else {}
+        want = {"nerf": {"W": 256, "D": 8, "skips": [4]}, "xyz_encoder": {"freq": 10},
+                "dir_encoder": {"freq": 4}}
+        for blk, keys in want.items():
+            got = net_cfg.get(blk, {}) if hasattr(net_cfg, "get") else {}
+            for k, v in keys.items():
+                if k not in got:
+                    continue
+                g = list(got[k]) if isinstance(v, list) else got[k]
+                if g != v:
+                    raise NotImplementedError(f"cfg.network.{blk}.{k}={got[k]!r}: the HIP "
+                                              f"kernels implement {v!r} only")
+        for prefix, mod in (("model", self.coarse_model), ("model_fine", self.fine_model)):
+            sd = mod.state_dict()
+            for name, fout, fin in layer_shapes(prefix):
+                w = sd.get(name[len(prefix) + 1:] + ".weight")
+                if w is None or tuple(w.shape) != (fout, fin):
+                    raise NotImplementedError(
+                        f"{name}.weight: shape {None if w is None else tuple(w.shape)} != "
+                        f"{(fout, fin)} (the lego 8x256 topology the HIP kernels implement)")
+
     # ------------------------------------------------------------- ESS state
     def _initialize_occupancy_grid(self):
-        """Reference VR:830-873: sphere (|c| <= 1.2 in [-1,1]^3) OR rand < 0.1."""
+        """Reference VR:830-873: sphere (|c| <= 1.2 in [-1,1]^3) OR rand < 0.1. Only
+        with ESS on: the reference's version returns at once otherwise (:832-833),
+        so its torch.rand draw happens exactly when it does here."""
         res = self.occupancy_grid_resolution
         ax = torch.arange(res, device=self.device, dtype=torch.float32) / (res - 1) * 2.0 - 1.0
-        gx, gy, gz = torch.meshgrid(ax, ax, ax, indexing="ij")
-        sphere = torch.sqrt(gx * gx + gy * gy + gz * gz) <= 1.2
+        coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1)
+        sphere = torch.norm(coords, dim=-1) <= 1.2
         noise = torch.rand((res, res, res), device=self.device) < 0.1
         self.occupancy_grid = sphere | noise
         self.ess_skip_threshold = 0.5
@@ -120,10 +150,11 @@ class Renderer:
 
     # ------------------------------------------------------------- render
     def render(self, batch):
-        """Reference VR:89-107 -> _render_pytorch contract (HIP path only)."""
+        """Reference VR:89-107 -> _render_pytorch contract (HIP path only). With
+        the network in training mode and autograd on (trainers/nerf.py:20-37),
+        the maps carry gradients into net.model / net.model_fine."""
         if torch.is_grad_enabled() and self.net.training:
-            raise NotImplementedError("training-mode render (backward through the MLP) is "
-                                      "the next row of the build; wrap eval in torch.no_grad()")
+            return self._render_train(batch)
         H, W = int(batch["H"]), int(batch["W"])
         pose = torch.as_tensor(batch["pose"]).reshape(-1, 4, 4)[0].float()
         K = torch.as_tensor(batch["intrinsics"]).reshape(-1, 3, 3)[0].float()
@@ -141,6 +172,26 @@ class Renderer:
         for k, v in res.items():
             out[k] = v.view(H, W, 3) if k.startswith("rgb") else v.view(H, W)
         return out
+
+    def _render_train(self, batch):
+        """Training-mode render (VR:109-268 with self.net.training): rays and
+        coarse depths from the HIP kernels, both MLPs forward + backward on the
+        x3 MFMA training kernels (cfg ``train_mlp``: "x3", default, or "torch"),
+        compositing / importance sampling / ERT in torch autograd; the reference's
+        RNG order per 2048-ray chunk (perturb draw, then fine u) and its ESS/ERT
+        chunk semantics (nerfhip.train.render_rays_train)."""
+        from nerfhip.train import query, render_rays_train
+        from nerfhip.train_mlp import query_x3
+        H, W = int(batch["H"]), int(batch["W"])
+        pose = torch.as_tensor(batch["pose"]).reshape(-1, 4, 4)[0].float()
+        K = torch.as_tensor(batch["intrinsics"]).reshape(-1, 3, 3)[0].float()
+        rays_o, rays_d = self.pipeline.camera_rays(H, W, pose, K)
+        qf = query if getattr(cfg, "train_mlp", "x3") == "torch" else query_x3
+        res = render_rays_train(self.pipeline, self.coarse_model,
+                                self.fine_model if self.N_importance > 0 else None,
+                                rays_o, rays_d, float(self.perturb), qf)
+        return {k: v.view(H, W, 3) if k.startswith("rgb") else v.view(H, W)
+                for k, v in res.items()}
 
     # ------------------------------------------------------------- paths
     def generate_spiral_poses(self, poses, n_frames=None, n_rots=2, zrate=0.5):
@@ -174,8 +225,54 @@ class Renderer:
             disps.append(np.clip(disp, 0, mx if mx > 0 else 1.0))
         return np.array(rgbs), np.array(disps)
 
-    def render_novel_view_sequence(self, *a, **kw):
-        raise NotImplementedError("writing image/video sequences is outside the render hot path")
+    def render_novel_view_sequence(self, poses, hwf, output_dir, exp_name, iteration=0,
+                                   intrinsics=None, render_type="spiral"):
+        """VR:511-616: render the spiral (cfg.render_num frames) or the given poses
+        through render(batch) under no_grad, clip rgb to [0,1] and disp to
+        [0, max], convert to 8 bit like the reference, and write
+        ``<output_dir>/novel_views/view%04d_{rgb,disp}.png`` (PIL instead of cv2;
+        skipped when output_dir is None). The 8-bit frames are also kept in
+        ``self.last_sequence`` = (rgb [N,H,W,3] uint8, disp [N,H,W] uint8).
+        Video encoding is out of scope: the returned video path is None. Errors
+        propagate (the reference prints them and goes on)."""
+        import os
+        if render_type == "spiral":
+            render_poses = self.generate_spiral_poses(poses, n_frames=getattr(cfg, "render_num",
+                                                                              120))
+        else:
+            render_poses = poses.cpu().numpy() if torch.is_tensor(poses) else np.asarray(poses)
+        H, W, focal = hwf
+        if intrinsics is None:
+            Kt = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]],
+                              dtype=torch.float32, device=self.device)
+        else:
+            Kt = torch.as_tensor(intrinsics).to(self.device)
+        images_dir = None
+        if output_dir is not None:
+            images_dir = os.path.join(output_dir, "novel_views")
+            os.makedirs(images_dir, exist_ok=True)
+        rgb8s, disp8s = [], []
+        with torch.no_grad():
+            for i, pose in enumerate(render_poses):
+                batch = {"pose": torch.as_tensor(np.asarray(pose), dtype=torch.float32)
+                         .to(self.device)[None], "intrinsics": Kt[None], "H": H, "W": W}
+                ret = self.render(batch)
+                key = "rgb_map" if "rgb_map" in ret else "rgb_map_0"
+                rgb = np.clip(ret[key].cpu().numpy(), 0, 1)
+                disp = ret[key.replace("rgb", "disp")].cpu().numpy()
+                mx = np.max(disp)
+                disp = np.clip(disp, 0, mx if mx > 0 else 1.0)
+                mx = np.max(disp)
+                rgb8 = (255 * rgb).astype(np.uint8)
+                disp8 = (255 * disp / mx if mx > 0 else disp).astype(np.uint8)
+                rgb8s.append(rgb8)
+                disp8s.append(disp8)
+                if images_dir is not None:
+                    from PIL import Image
+                    Image.fromarray(rgb8).save(os.path.join(images_dir, f"view{i:04d}_rgb.png"))
+                    Image.fromarray(disp8).save(os.path.join(images_dir, f"view{i:04d}_disp.png"))
+        self.last_sequence = (np.stack(rgb8s), np.stack(disp8s))
+        return images_dir, None
 
     def create_video_from_result_images(self, *a, **kw):
         raise NotImplementedError("video encoding is outside the render hot path")

@@ -7,7 +7,13 @@ fine-sampling u ~ U[0,1), gradients through _sample_fine, volume_renderer.py:
 draw), the losses and, per parameter, the gradient's float64 norm and sum plus
 its first 64 values. Nothing from the reference's source is stored.
 
-    python tests/golden/make_train_golden.py
+    python tests/golden/make_train_golden.py          # t1 and t2
+
+t1: ESS/ERT off, 8x16 crop. t2: ESS + ERT on (lego.yaml:96-99) over a 48x48 crop
+(2304 rays = one full 2048-ray chunk + 256), a deterministic occupancy grid and
+call counter 0 (the grid self-updates from chunk 0's coarse call), dense weights
+so that some rays terminate and the chunk-wide argmax rule (VR:1115-1123) fires;
+it also stores all 8 maps, the updated grid and the counter.
 """
 from __future__ import annotations
 
@@ -21,7 +27,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as mg  # noqa: E402
 
-SPEC = dict(H=8, W=16, res=800, x0=392, y0=396, frame=0, w=(5, 2.0, 0.5))
+SPECS = {
+    "t1_train_step": dict(H=8, W=16, res=800, x0=392, y0=396, frame=0, w=(5, 2.0, 0.5)),
+    "t2_train_ess_ert": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                             ess_ert=True, grid=dict(seed=4, radius=0.5, noise=0.01), counter=0),
+}
 
 
 def synthetic_gt(H, W):
@@ -33,15 +43,21 @@ def synthetic_gt(H, W):
 
 def main():
     cfg, Network, vr = mg._import_reference()
-    import torch
     with open(os.path.join(mg.REF, "data", "nerf_synthetic", "lego", "transforms_test.json")) as f:
         meta = json.load(f)
+    for name, spec in SPECS.items():
+        capture(name, spec, cfg, Network, vr, meta)
+
+
+def capture(name, SPEC, cfg, Network, vr, meta):
+    import torch
     frames, angle = meta["frames"], float(meta["camera_angle_x"])
     cfg.task_arg.N_importance = 128
     cfg.task_arg.perturb = 1
     cfg.task_arg.lindisp = False
-    cfg.enable_ess = False
-    cfg.enable_ert = False
+    cfg.enable_ess = bool(SPEC.get("ess_ert", False))
+    cfg.enable_ert = bool(SPEC.get("ess_ert", False))
+    cfg.ert_threshold = 0.01
     seed, gain, ab = SPEC["w"]
     params = mg.make_params(seed, gain, ab)
     net = Network()
@@ -49,6 +65,11 @@ def main():
     net.train()
     rend = vr.Renderer(net)
     rend.use_cuda_kernels = False
+    if "grid" in SPEC:
+        g = SPEC["grid"]
+        rend.occupancy_grid = torch.from_numpy(
+            mg.make_occupancy_grid(g["seed"], 128, g["radius"], g["noise"]).copy())
+        rend.grid_update_counter = SPEC.get("counter", 0)
     pose, K = mg._camera(SPEC, frames, angle)
     H, W = SPEC["H"], SPEC["W"]
     gt = synthetic_gt(H, W)
@@ -89,7 +110,17 @@ def main():
                u=np.concatenate(u, 0)[:n], loss=np.float64(loss.item()),
                loss_coarse=np.float64(loss_c.item()), loss_fine=np.float64(loss_f.item()),
                rgb_map_0=out["rgb_map_0"].detach().numpy().reshape(n, 3),
-               rgb_map=out["rgb_map"].detach().numpy().reshape(n, 3))
+               rgb_map=out["rgb_map"].detach().numpy().reshape(n, 3),
+               enable_ess=cfg.enable_ess, enable_ert=cfg.enable_ert,
+               ert_threshold=np.float64(cfg.ert_threshold))
+    for k, v in out.items():
+        rec["out_" + k] = v.detach().numpy()
+    if "grid" in SPEC:
+        g = SPEC["grid"]
+        rec.update(grid_seed=g["seed"], grid_radius=g["radius"], grid_noise=g["noise"],
+                   grid_counter_in=SPEC.get("counter", 0),
+                   grid_counter_out=rend.grid_update_counter,
+                   grid_out_packed=np.packbits(rend.occupancy_grid.numpy().reshape(-1)))
     names = []
     for k, p in net.named_parameters():
         g = p.grad.detach().double()
@@ -101,7 +132,7 @@ def main():
             rec["gcnorm__" + k] = np.float64(coarse_only[k].norm().item())
             rec["gchead__" + k] = coarse_only[k].numpy().reshape(-1)[:64].copy()
     rec["param_names"] = np.array(names)
-    path = os.path.join(HERE, "t1_train_step.npz")
+    path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **rec)
     print("wrote", path, "loss", loss.item(), "params", len(names))
 

@@ -14,6 +14,8 @@ from nerfhip import dist as nd
 
 
 def fake_render(p0, n, with_fine=True):
+    if n == 0:
+        return {}
     p = torch.arange(p0, p0 + n, dtype=torch.float32)
     out = {"rgb_map_0": torch.stack([p, p + 0.25, p + 0.5], -1), "disp_map_0": -p,
            "acc_map_0": p * 0.5, "depth_map_0": p + 3.0}

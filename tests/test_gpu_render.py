@@ -385,3 +385,59 @@ def test_renderer_spiral_render_path(dev):
         one = rend.render(batch)
     np.testing.assert_array_equal(rgbs[1], np.clip(one["rgb_map"].cpu().numpy(), 0, 1))
     reset()
+
+
+def _band_frame(dev, H, W, world, counter0, grid, params, prec="f16x3"):
+    """render_frame_sharded's band / pack / unpack path with world ranks rendered
+    one after another on one device (each rank: its own pipeline, same start
+    state); returns the assembled frame and every rank's final grid + counter."""
+    from nerfhip import dist as nd
+    cams = load("lego_test_cameras")
+    f = 0.5 * 800 / np.tan(0.5 * float(cams["camera_angle_x"]))
+    K = np.array([[f, 0, 400 - 352], [0, f, 400 - 352], [0, 0, 1]], np.float32)
+    pose = cams["poses"][0]
+    parts, states = [], []
+    n_pad = None
+    for r in range(world):
+        pipe = _pipe(dev, N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
+                     ert_threshold=0.01, mlp_precision=prec)
+        pipe.set_weights(params)
+        pipe.set_grid(grid)
+        pipe.grid_update_counter = counter0
+        p0, n, n_pad = nd.band(H, W, r, world, chunk_aligned=True)
+        maps = pipe.render_band(H, W, pose, K, p0, n)
+        parts.append(nd.pack_maps(maps, n, n_pad, dev)[:n])
+        states.append((pipe.grid.clone(), pipe.grid_update_counter))
+    full = torch.cat(parts, 0)
+    return nd.unpack_maps(full, H, W, set(nd.MAP_ORDER)), states, (pose, K)
+
+
+@pytest.mark.parametrize("counter0", [496, 497])
+def test_sharded_c4_bands_equal_one_pass_frame(dev, counter0):
+    """C4 (ESS + ERT) split into chunk-aligned bands for 2/4/8 ranks: bit-exactly
+    the one-pass frame, whose ESS grid self-updates mid-frame (counter0 496: the
+    coarse call of chunk 2; 497: the fine call of chunk 1, VR:1147-1157), and
+    every rank ends with the sequential loop's grid and counter."""
+    from nerfhip.synthetic import make_occupancy_grid, make_params
+    H = W = 96                                  # 9216 rays = 4.5 chunks
+    params = make_params(0, 3.0, 1.0)
+    grid = make_occupancy_grid(4, 128, 0.5, 0.01)
+    ref, st1, (pose, K) = _band_frame(dev, H, W, 1, counter0, grid, params)
+    one = _pipe(dev, N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
+                ert_threshold=0.01)
+    one.set_weights(params)
+    one.set_grid(grid)
+    one.grid_update_counter = counter0
+    direct = one.render_image(H, W, pose, K)
+    assert not torch.equal(one.grid, torch.as_tensor(grid).to(dev).to(torch.uint8).view(-1))
+    for k in ref:
+        assert torch.equal(torch.nan_to_num(ref[k].reshape(-1), 7.0),
+                           torch.nan_to_num(direct[k].reshape(-1), 7.0)), k
+    for world in (2, 4, 8):
+        got, states, _ = _band_frame(dev, H, W, world, counter0, grid, params)
+        for k in ref:
+            assert torch.equal(torch.nan_to_num(got[k], 7.0), torch.nan_to_num(ref[k], 7.0)), \
+                (world, k)
+        for g, c in states:
+            assert c == one.grid_update_counter
+            assert torch.equal(g, one.grid)

@@ -78,3 +78,130 @@ def test_steps_reduce_loss(dev, mlp):
     assert last < 0.8 * first
     for p in tr.parameters():                       # clip_grad_value_(40) held
         assert p.grad is None or p.grad.abs().max() <= 40.0
+
+
+# ------------------------------------------------------------------ the plugin
+def _plugin_train_render(dev, name, mlp):
+    """Renderer(net).render(batch) in training mode, as trainers/nerf.py:20-37
+    calls it, with the reference's recorded torch.rand draws replayed in its
+    order (per 2048-ray chunk: perturb t_rand, then the fine u)."""
+    from goldlib import grid_of
+    from nerfhip.synthetic import load_into_network
+    from src.config import cfg, reset
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    z = load(name)
+    reset()
+    cfg.task_arg.perturb = 1
+    cfg.enable_ess = bool(z["enable_ess"])
+    cfg.enable_ert = bool(z["enable_ert"])
+    cfg.ert_threshold = float(z["ert_threshold"])
+    cfg.train_mlp = mlp
+    net = Network().to(dev)
+    load_into_network(net, params_of(z))
+    net.train()
+    rend = Renderer(net)
+    if "grid_seed" in z:
+        rend.occupancy_grid = grid_of(z)
+        rend.grid_update_counter = int(z["grid_counter_in"])
+    n = int(z["H"]) * int(z["W"])
+    draws = []
+    for c0 in range(0, n, 2048):
+        draws += [z["t_rand"][c0:c0 + 2048], z["u"][c0:c0 + 2048]]
+    it = iter(draws)
+    orig = torch.rand
+
+    def replay(size, *a, device=None, **kw):
+        arr = next(it)
+        assert tuple(arr.shape) == tuple(size), (arr.shape, size)
+        return torch.from_numpy(np.ascontiguousarray(arr)).to(device)
+    batch = {"H": int(z["H"]), "W": int(z["W"]), "pose": torch.from_numpy(z["pose"])[None],
+             "intrinsics": torch.from_numpy(z["K"])[None]}
+    torch.rand = replay
+    try:
+        out = rend.render(batch)
+    finally:
+        torch.rand = orig
+        reset()
+    assert next(it, None) is None, "not every recorded draw was consumed"
+    return z, net, rend, out
+
+
+@pytest.mark.parametrize("name", ["t1_train_step", "t2_train_ess_ert"])
+@pytest.mark.parametrize("mlp", ["x3", "torch"])
+def test_plugin_training_render_matches_reference(dev, name, mlp):
+    """North_star drop-in for train.py: the plugin's training-mode render gives the
+    reference's coarse maps (1e-5), losses and gradients (coarse loss alone 1e-3
+    of each tensor's norm; full loss: norms within 5 %, as the trainer test),
+    with ERT/ESS (t2) also the grid self-update and call counter exactly."""
+    from goldlib import rel_err
+    z, net, rend, out = _plugin_train_render(dev, name, mlp)
+    H, W = int(z["H"]), int(z["W"])
+    n = H * W
+    assert out["rgb_map"].shape == (H, W, 3) and out["depth_map"].shape == (H, W)
+    assert out["rgb_map_0"].requires_grad and out["rgb_map"].requires_grad
+    g = {k: v.detach().cpu().numpy() for k, v in out.items()}
+    assert max_err(g["rgb_map_0"].reshape(n, 3), z["rgb_map_0"]) < 1e-5
+    if "out_acc_map_0" in z:
+        assert max_err(g["acc_map_0"], z["out_acc_map_0"]) < 1e-5
+        assert rel_err(g["depth_map_0"], z["out_depth_map_0"]) < 1e-5
+        assert np.array_equal(np.isnan(g["disp_map_0"]), np.isnan(z["out_disp_map_0"]))
+    if "grid_out_packed" in z:
+        assert rend.grid_update_counter == int(z["grid_counter_out"])
+        assert np.array_equal(np.packbits(rend.occupancy_grid.cpu().numpy().reshape(-1)),
+                              z["grid_out_packed"])
+    gt = torch.from_numpy(z["gt"].reshape(-1, 3)).to(dev)
+    loss_c = torch.nn.functional.mse_loss(out["rgb_map_0"].reshape(-1, 3), gt)
+    loss_f = torch.nn.functional.mse_loss(out["rgb_map"].reshape(-1, 3), gt)
+    assert abs(loss_c.item() - float(z["loss_coarse"])) <= 1e-6 * max(1.0, float(z["loss_coarse"]))
+    assert abs((loss_c + loss_f).item() - float(z["loss"])) / float(z["loss"]) < 1e-3
+    params = dict(net.named_parameters())
+    net.zero_grad(set_to_none=True)
+    loss_c.backward(retain_graph=True)
+    for k, p in params.items():
+        if "gcnorm__" + k not in z:
+            continue
+        ref = float(z["gcnorm__" + k])
+        gk = p.grad.detach().double().cpu()
+        assert abs(gk.norm().item() - ref) <= 1e-3 * ref + 1e-12, k
+        assert np.abs(gk.reshape(-1)[:64].numpy() - z["gchead__" + k]).max() <= 1e-3 * ref + 1e-12, k
+    net.zero_grad(set_to_none=True)
+    (loss_c + loss_f).backward()
+    for k in [str(s) for s in z["param_names"]]:
+        ref_norm = float(z["gnorm__" + k])
+        assert abs(params[k].grad.detach().double().norm().item() - ref_norm) <= \
+            5e-2 * ref_norm + 1e-9, k
+
+
+def test_plugin_novel_view_sequence(dev, tmp_path):
+    """render_novel_view_sequence (VR:511-616): one 8-bit frame per spiral pose,
+    equal to render(batch) of that pose; PNGs written; no video (out of scope)."""
+    from nerfhip.synthetic import load_into_network
+    from src.config import cfg, reset
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    z = load("f1_c2_crop")
+    reset()
+    cfg.task_arg.perturb = 0
+    cfg.enable_ess = False
+    cfg.enable_ert = False
+    cfg.render_num = 3
+    net = Network().to(dev)
+    load_into_network(net, params_of(z))
+    net.eval()
+    rend = Renderer(net)
+    poses = load("lego_test_cameras")["poses"]
+    H, W, focal = 10, 14, 20.0
+    images_dir, video = rend.render_novel_view_sequence(poses, (H, W, focal), str(tmp_path), "t")
+    rgb8, disp8 = rend.last_sequence
+    assert rgb8.shape == (3, H, W, 3) and disp8.shape == (3, H, W) and video is None
+    import os
+    assert sorted(os.listdir(images_dir))[:2] == ["view0000_disp.png", "view0000_rgb.png"]
+    sp = rend.generate_spiral_poses(poses, n_frames=3)
+    K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
+    with torch.no_grad():
+        one = rend.render({"H": H, "W": W, "pose": torch.from_numpy(sp[2].astype(np.float32))[None],
+                           "intrinsics": torch.from_numpy(K)[None]})
+    ref = (255 * np.clip(one["rgb_map"].cpu().numpy(), 0, 1)).astype(np.uint8)
+    np.testing.assert_array_equal(rgb8[2], ref)
+    reset()

@@ -78,3 +78,30 @@ def test_train_math_matches_reference_backward():
             assert abs(q.grad.double().norm().item() - ref) <= 1e-5 * ref, name
             np.testing.assert_allclose(q.grad.reshape(-1)[:64].numpy(), z["ghead__" + name],
                                        atol=1e-5 * ref, rtol=0)
+
+
+@pytest.mark.parametrize("white", [True, False])
+def test_composite_ert_matches_oracle_per_chunk(white):
+    """nerfhip.train.composite_ert (the training-mode ERT, autograd) vs the
+    oracle's VR:1089-1133 over 2048-ray chunks: a chunk with terminating rays
+    (argmax quirk), one where a single ray terminates, one where none does."""
+    rng = np.random.default_rng(3)
+    n, S = 2048 * 2 + 300, 48
+    raw = rng.normal(0, 2, (n, S, 4)).astype(np.float32)
+    raw[..., 3] = rng.normal(2.0, 3.0, (n, S)).astype(np.float32)
+    raw[2048:, :, 3] = -5.0
+    raw[2048 + 9, :, 3] = 40.0
+    z = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    t_raw = torch.from_numpy(raw).requires_grad_(True)
+    got = T.composite_ert(t_raw, torch.from_numpy(z), torch.from_numpy(d), 0.01, white)
+    for c0 in range(0, n, 2048):
+        sl = slice(c0, min(n, c0 + 2048))
+        ref = O.raw2outputs_ert(raw[sl], z[sl], d[sl], 0.01, white)
+        for g, r in zip(got, ref):
+            np.testing.assert_allclose(g.detach().numpy()[sl], r, atol=2e-6, rtol=1e-5)
+    got[0].sum().backward()
+    assert torch.isfinite(t_raw.grad).all()
+    g1 = torch.cat([t_raw.grad[2048:2048 + 9], t_raw.grad[2048 + 10:4096]])
+    assert (g1 == 0).all()          # chunk 1: every other ray's weights zeroed (quirk 1)
