@@ -5,7 +5,9 @@
   when the render size differs (:77-84);
 * PSNR: both images clipped to [0, 1], mse = mean((pred - gt)^2),
   psnr = -10 log10(mse) (inf for mse = 0) (src/evaluators/nerf.py:465-473,
-  :50-58), averaged over frames (:502-504).
+  :50-58), averaged over frames (:502-504);
+* SSIM: skimage's structural_similarity as the evaluator calls it (:65-107),
+  restated (scikit-image is not in this image).
 """
 from __future__ import annotations
 
@@ -63,18 +65,66 @@ def load_packed(path, H=None, W=None, indices=None):
 
 
 def psnr(pred, gt):
-    pred = np.clip(np.asarray(pred, np.float64), 0, 1)
-    gt = np.clip(np.asarray(gt, np.float64), 0, 1)
+    """evaluators/nerf.py:463-473 + psnr_metric (:24-63): both images clipped to
+    [0, 1] in their own dtype (float32 renders), mse = np.mean((pred - gt)^2) in
+    that dtype, psnr = 20 log10(1) - 10 log10(mse) (inf for mse = 0)."""
+    pred = np.clip(np.asarray(pred), 0, 1)
+    gt = np.clip(np.asarray(gt), 0, 1)
     mse = np.mean((pred - gt) ** 2)
-    return float("inf") if mse == 0 else float(-10.0 * np.log10(mse))
+    if mse == 0:
+        return float("inf")
+    return float(20 * np.log10(1.0) - 10 * np.log10(mse))
 
 
-def evaluate(render, frames):
-    """frames: iterable of (pose, K, gt [H,W,3]); render(H, W, pose, K) -> rgb
-    [H*W,3] or [H,W,3]. Returns per-frame PSNRs and their mean."""
+def ssim(pred, gt, win_size=None, data_range=1.0):
+    """evaluators/nerf.py:65-107: skimage.metrics.structural_similarity(pred, gt,
+    win_size=min(7, H, W), data_range=1.0, channel_axis=2) on the [0, 1]-clipped
+    images. scikit-image is absent here and unpinned by the reference
+    (requirements.txt), so this restates its published default algorithm (Wang
+    et al. 2004 as skimage implements it): uniform win x win window
+    (scipy.ndimage.uniform_filter), K1 = 0.01, K2 = 0.03, sample covariance
+    (N / (N - 1)), the SSIM map cropped by (win - 1) / 2 on every side and
+    averaged, then averaged over the channels; computed in float64. Parity with
+    skimage itself is unpinned."""
+    from scipy.ndimage import uniform_filter
+    X = np.clip(np.asarray(pred, np.float64), 0, 1)
+    Y = np.clip(np.asarray(gt, np.float64), 0, 1)
+    if X.shape != Y.shape:
+        raise ValueError("ssim: images differ in shape")
+    if X.ndim == 2:
+        X, Y = X[..., None], Y[..., None]
+    if win_size is None:
+        win_size = min(7, X.shape[0], X.shape[1])
+    if win_size % 2 == 0 or win_size > min(X.shape[0], X.shape[1]):
+        raise ValueError("ssim: win_size must be odd and fit the image")
+    C1, C2 = (0.01 * data_range) ** 2, (0.03 * data_range) ** 2
+    cov = win_size ** 2 / (win_size ** 2 - 1.0)
+    pad = (win_size - 1) // 2
     vals = []
+    for c in range(X.shape[2]):
+        x, y = X[..., c], Y[..., c]
+        f = lambda a: uniform_filter(a, size=win_size)   # noqa: E731
+        ux, uy = f(x), f(y)
+        vx = cov * (f(x * x) - ux * ux)
+        vy = cov * (f(y * y) - uy * uy)
+        vxy = cov * (f(x * y) - ux * uy)
+        S = ((2 * ux * uy + C1) * (2 * vxy + C2)) / ((ux * ux + uy * uy + C1) * (vx + vy + C2))
+        vals.append(S[pad:S.shape[0] - pad, pad:S.shape[1] - pad].mean())
+    return float(np.mean(vals))
+
+
+def evaluate(render, frames, with_ssim=True):
+    """frames: iterable of (pose, K, gt [H,W,3]); render(H, W, pose, K) -> rgb
+    [H*W,3] or [H,W,3]. Per-frame PSNR (and SSIM) and their means
+    (evaluators/nerf.py:495-517)."""
+    vals, ssims = [], []
     for pose, K, gt in frames:
         H, W = gt.shape[:2]
         rgb = np.asarray(render(H, W, pose, K)).reshape(H, W, 3)
         vals.append(psnr(rgb, gt))
-    return {"psnr": vals, "psnr_mean": float(np.mean(vals)) if vals else float("nan")}
+        if with_ssim:
+            ssims.append(ssim(rgb, gt))
+    res = {"psnr": vals, "psnr_mean": float(np.mean(vals)) if vals else float("nan")}
+    if with_ssim:
+        res.update(ssim=ssims, ssim_mean=float(np.mean(ssims)) if ssims else float("nan"))
+    return res

@@ -41,3 +41,39 @@ def test_psnr_formula_and_average():
     frames = [(None, None, gt), (None, None, gt)]
     res = E.evaluate(lambda H, W, pose, K: pred.reshape(-1, 3), frames)
     assert res["psnr"] == [pytest.approx(20.0, abs=1e-5)] * 2 and abs(res["psnr_mean"] - 20) < 1e-5
+
+
+def _ssim_bruteforce(x, y, win=7, C1=1e-4, C2=9e-4):
+    """Window-by-window SSIM over the interior windows (the ones skimage keeps
+    after cropping), sample (N-1) covariance, mean over pixels then channels."""
+    H, W, C = x.shape
+    p = win // 2
+    out = []
+    for c in range(C):
+        vals = []
+        for i in range(p, H - p):
+            for j in range(p, W - p):
+                a = x[i - p:i + p + 1, j - p:j + p + 1, c].ravel()
+                b = y[i - p:i + p + 1, j - p:j + p + 1, c].ravel()
+                ma, mb = a.mean(), b.mean()
+                va, vb = a.var(ddof=1), b.var(ddof=1)
+                cab = ((a - ma) * (b - mb)).sum() / (a.size - 1)
+                vals.append(((2 * ma * mb + C1) * (2 * cab + C2)) /
+                            ((ma * ma + mb * mb + C1) * (va + vb + C2)))
+        out.append(np.mean(vals))
+    return float(np.mean(out))
+
+
+def test_ssim_matches_windowed_definition():
+    rng = np.random.default_rng(0)
+    gt = rng.random((20, 17, 3)).astype(np.float32)
+    pred = np.clip(gt + rng.normal(0, 0.05, gt.shape), 0, 1).astype(np.float32)
+    assert abs(E.ssim(pred, gt) - _ssim_bruteforce(pred.astype(np.float64),
+                                                   gt.astype(np.float64))) < 1e-12
+    assert E.ssim(gt, gt) == pytest.approx(1.0, abs=1e-12)
+    assert E.ssim(pred, gt) < 1.0
+    assert E.ssim(pred[:5, :5], gt[:5, :5]) == pytest.approx(
+        _ssim_bruteforce(pred[:5, :5].astype(np.float64), gt[:5, :5].astype(np.float64), win=5),
+        abs=1e-12)
+    res = E.evaluate(lambda H, W, pose, K: pred, [(None, None, gt)])
+    assert res["ssim_mean"] == pytest.approx(E.ssim(pred, gt))
