@@ -5,21 +5,27 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One step = one full 800x800 frame (640,000 rays, 64 coarse + 192 fine MLP
-evaluations per ray) of the lego test camera (poses cycled over the 200 test
-views), split into row bands across the ranks, maps all-gathered over RCCL.
-Inputs (packed weights, z tables) are resident in HBM before timing starts.
-Weights are synthetic (deterministic generator, no checkpoint offline).
+evaluations per ray) of a lego test view (views 0, 8, ..., 192 cycled), split
+into row bands across the ranks, maps all-gathered over RCCL. Inputs (packed
+weights, z tables) are resident in HBM before timing starts. Weights: the lego
+checkpoint trained by tools/train_lego.py (checkpoints/lego) when present,
+else the deterministic synthetic generator (--synthetic forces it).
 
 The headline run uses the default MLP arithmetic (--precision f16x3: FP32
 operands as 3-term FP16 splits on FP16 MFMA with FP32 accumulation, held to the
 same parity gates as FP32); the same frames are then timed with
 the FP32-MFMA kernel and reported under "fp32_mfma".
 
-Prints one JSON line (rank 0). Also reports the fused MLP kernel's roofline
-(its HIP-event-timed launches: executed MFMA FLOP/s vs the dense MFMA peak of
-the type it runs on, plus the algorithmic FP32 FLOP/s) and the CPU oracle
-(numpy restatement of the reference) timed on a bounded strip of the same
-frame, with the GPU-vs-oracle parity on that strip.
+Prints one JSON line (rank 0) with, besides the contract keys:
+  roofline        the fused MLP kernel's HIP-event-timed launches: executed MFMA
+                  FLOP/s vs the dense peak of the type it runs on (+ algorithmic)
+  parity          GPU vs the parity oracle (oracle/nerf_oracle.py) on a strip
+  cpu_baseline    the reference's CPU path (torch-CPU restatement,
+                  oracle/torch_render.py) timed on this host's cores on a strip
+  psnr_vs_gt      evaluator PSNR/SSIM of the HIP render of the packed lego test
+                  views vs ground truth (data/lego/test.npz), and |dPSNR| HIP vs
+                  oracle on the strip
+  c3_train_step   BASELINE configs[2]: the 1024-ray training step, timed
 """
 import argparse
 import json
@@ -43,12 +49,18 @@ X3_EXEC_FLOP_PER_SAMPLE = 2 * 3 * 528384
 METRIC = "Mrays/s + ms/frame, lego 800x800 (64c+128f); PSNR vs ref"
 
 
+GT_STRIDE = 8          # tools/pack_lego.py: data/lego/test.npz = test frames 0, 8, ..., 192
+DEFAULT_CKPT = os.path.join(REPO, "checkpoints", "lego")
+GT_PATH = os.path.join(REPO, "data", "lego", "test.npz")
+
+
 def lego_camera(H, W, idx):
+    """Test view GT_STRIDE * (idx mod 25): the frames whose ground truth is packed."""
     cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
     poses, angle = cams["poses"], float(cams["camera_angle_x"])
     focal = 0.5 * W / np.tan(0.5 * angle)            # blender.py:41-42
     K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
-    return poses[idx % len(poses)], K
+    return poses[(GT_STRIDE * idx) % len(poses)], K
 
 
 def main():
@@ -69,8 +81,12 @@ def main():
                          "c3: train step, 1024 rays/rank (configs[2]); "
                          "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99)")
     ap.add_argument("--checkpoint", default=None,
-                    help="trained weights (a reference-format .pth or model dir) instead of "
-                         "the synthetic generator")
+                    help="trained weights (a reference-format .pth or model dir); default: "
+                         "checkpoints/lego (trained by tools/train_lego.py) when present")
+    ap.add_argument("--synthetic", action="store_true",
+                    help="synthetic generator weights even when the trained checkpoint exists")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 train-step sub-record of the default run")
     ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
                     help="c3: the MLPs on the x3 MFMA training kernels (default) or as torch "
                          "modules (FP32 hipBLASLt GEMMs)")
@@ -96,10 +112,15 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     H, W = args.H, args.W
-    if args.checkpoint:
-        from nerfhip.checkpoint import network_params
-        params = {k: v.numpy() for k, v in network_params(args.checkpoint).items()}
-        data = f"checkpoint {args.checkpoint}, lego test cameras"
+    ckpt = args.checkpoint
+    if ckpt is None and not args.synthetic and os.path.exists(DEFAULT_CKPT):
+        ckpt = DEFAULT_CKPT
+    if ckpt:
+        from nerfhip.checkpoint import load_checkpoint, network_params, resolve
+        params = {k: v.numpy() for k, v in network_params(ckpt).items()}
+        step = load_checkpoint(resolve(ckpt)).get("epoch")
+        data = (f"lego checkpoint {os.path.relpath(resolve(ckpt), REPO)} (trained on the 100 "
+                f"lego train views by tools/train_lego.py, {step} steps), lego test cameras")
     else:
         params = make_params(0, 2.0, 0.0)
         data = "synthetic weights (deterministic generator, seed 0, gain 2), lego test cameras"
@@ -180,23 +201,37 @@ def main():
             result["cpu_baseline"], result["parity"] = cpu_baseline_c4(
                 make_pipe(args.precision), H, W, params, args.cpu_rows)
         else:
-            result["cpu_baseline"], result["parity"] = cpu_baseline(pipe, H, W, params,
-                                                                    args.cpu_rows)
+            result["parity"] = oracle_parity(pipe, H, W, params, args.cpu_rows)
+            result["cpu_baseline"] = torch_cpu_baseline(pipe, H, W, params, 2 * args.cpu_rows,
+                                                        result["parity"])
         result["psnr_vs_ref"] = result["parity"]["psnr_fine_rgb"]
+    if rank == 0 and world == 1 and not c4 and os.path.exists(GT_PATH):
+        result["psnr_vs_gt"] = psnr_vs_gt(pipe, H, W, result.get("parity"))
     del pipe
     if args.precision != "fp32" and not args.no_fp32_run:
         _, el32, roof32 = measure("fp32")
         result["fp32_mfma"] = {"value": rays / el32 / 1e6, "ms_per_step": el32 / args.steps * 1e3,
                                "dtype": DTYPES["fp32"], "roofline": roof32}
+    if world == 1 and not c4 and not args.no_c3:
+        c3 = bench_train(args, world, rank, dev, params, data, barrier, steps=20, warmup=3,
+                         emit=False)
+        result["c3_train_step"] = {k: c3[k] for k in ("metric", "value", "unit", "ms_per_step",
+                                                      "steps", "warmup", "dtype", "config",
+                                                      "roofline", "loss_last")}
+    if "parity" in result:
+        result["parity"].pop("_maps", None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def bench_train(args, world, rank, dev, params, data, barrier):
+def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmup=None,
+                emit=True):
     """C3: NerfTrainer.step on 1024 random lego-camera pixels per rank (synthetic
-    targets), data parallel over ranks (weak scaling)."""
+    targets), data parallel over ranks (weak scaling). emit=False: return the
+    record (the default bench run's "c3_train_step" sub-record) instead of
+    printing it."""
     import torch
     import torch.distributed as dist
     from nerfhip.render import NerfPipeline
@@ -219,14 +254,16 @@ def bench_train(args, world, rank, dev, params, data, barrier):
         target = torch.rand((nrays, 3), device=dev, generator=gen)
         return ro, rd, target
 
-    batches = [batch() for _ in range(args.warmup + args.steps)]
-    for i in range(args.warmup):
+    n_steps = args.steps if steps is None else steps
+    n_warm = args.warmup if warmup is None else warmup
+    batches = [batch() for _ in range(n_warm + n_steps)]
+    for i in range(n_warm):
         tr.step(*batches[i], group=group)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        losses = tr.step(*batches[args.warmup + i], group=group)
+    for i in range(n_steps):
+        losses = tr.step(*batches[n_warm + i], group=group)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -234,12 +271,12 @@ def bench_train(args, world, rank, dev, params, data, barrier):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_s = elapsed / args.steps
+    step_s = elapsed / n_steps
     flop = 3 * NerfPipeline.MLP_FLOP_PER_SAMPLE * nrays * (64 + 192)   # fwd + 2x bwd
     result = {
         "metric": "train step: Mrays/s (1024 rays/rank/step, 64c+128f) + ms/step",
-        "value": nrays * world * args.steps / elapsed / 1e6, "unit": "Mrays/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": nrays * world * n_steps / elapsed / 1e6, "unit": "Mrays/s",
+        "n_gpus": world, "steps": n_steps, "warmup": n_warm,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": DTYPES["f16x3"] if args.train_mlp == "x3" else "fp32",
@@ -252,10 +289,13 @@ def bench_train(args, world, rank, dev, params, data, barrier):
         "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
     }
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return result
 
 
 def train_roofline(mlp, flop, step_s):
@@ -327,16 +367,20 @@ def pmc_traffic(H, W, kernel="mlp_fused_kernel"):
     return best
 
 
-def cpu_baseline(pipe, H, W, params, rows):
-    """Oracle (numpy restatement of the reference renderer) on a bounded strip."""
+def _strip(H, W, rows):
+    r0 = max(0, H // 2 - rows // 2)
+    return r0, slice(r0 * W, (r0 + rows) * W)
+
+
+def oracle_parity(pipe, H, W, params, rows):
+    """GPU vs the parity oracle (oracle/nerf_oracle.py, the numpy restatement
+    pinned to the reference's golden renders) on a bounded strip of test view 0."""
     sys.path.insert(0, REPO)
     from oracle import nerf_oracle as O
     import torch
-    threads = _threads()
     pose, K = lego_camera(H, W, 0)
-    r0 = max(0, H // 2 - rows // 2)
+    r0, sl = _strip(H, W, rows)
     ro, rd = O.camera_rays(H, W, pose, K)
-    sl = slice(r0 * W, (r0 + rows) * W)
     cfg = O.RenderConfig(N_samples=64, N_importance=128)
     t0 = time.perf_counter()
     ref, _ = O.render(rows, W, pose, K, params, cfg, rays=(ro[sl], rd[sl]))
@@ -345,12 +389,77 @@ def cpu_baseline(pipe, H, W, params, rows):
     torch.cuda.synchronize()
     g = {k: v.cpu().numpy() for k, v in gpu.items()}
     n = rows * W
-    parity = {"strip_rows": [r0, r0 + rows], **_parity(g, ref, n)}
-    base = {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(threads),
-            "kind": "port", "seconds": t_cpu,
-            "sample": f"rows {r0}-{r0 + rows - 1} of lego test frame 0 at {H}x{W} "
-                      f"({n} rays, 64c+128f) rendered by oracle/nerf_oracle.py (numpy float32)"}
-    return base, parity
+    par = {"strip_rows": [r0, r0 + rows], "oracle_seconds": t_cpu, **_parity(g, ref, n)}
+    par["_maps"] = (g["rgb_map"].reshape(rows, W, 3), ref["rgb_map"].reshape(rows, W, 3))
+    return par
+
+
+def torch_cpu_baseline(pipe, H, W, params, rows, parity):
+    """The reference's CPU render path timed on this host's cores: the torch-CPU
+    restatement of _render_pytorch (oracle/torch_render.py: torch's own CPU
+    kernels, MKL GEMMs) on a bounded strip of test view 0, with its agreement
+    with the GPU on the same strip."""
+    sys.path.insert(0, REPO)
+    from oracle import torch_render as TR
+    import torch
+    pose, K = lego_camera(H, W, 0)
+    r0, sl = _strip(H, W, rows)
+    ro, rd = TR.camera_rays(H, W, pose, K)
+    t0 = time.perf_counter()
+    ref = TR.render_rays(ro[sl].contiguous(), rd[sl].contiguous(), params)
+    t_cpu = time.perf_counter() - t0
+    gpu = pipe.render_image(H, W, pose, K, p0=r0 * W, n=rows * W)
+    torch.cuda.synchronize()
+    g = {k: v.cpu().numpy() for k, v in gpu.items()}
+    n = rows * W
+    return {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(torch.get_num_threads()),
+            "kind": "port", "seconds": t_cpu, "host_cpus": os.cpu_count(),
+            "cpu_model": _cpu_model(),
+            "sample": f"rows {r0}-{r0 + rows - 1} of lego test view 0 at {H}x{W} ({n} rays, "
+                      f"64c+128f) rendered by oracle/torch_render.py (torch-CPU restatement of "
+                      f"_render_pytorch, {torch.get_num_threads()} threads)",
+            "agreement_with_gpu": {k: v for k, v in _parity(g, ref, n).items()}}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def psnr_vs_gt(pipe, H, W, parity):
+    """North_star "PSNR within 0.01 dB on lego": the evaluator's PSNR / SSIM
+    (evaluators/nerf.py:465-504; nerfhip.evaluate) of the HIP render of every
+    packed lego test view (data/lego/test.npz: frames 0, 8, ..., 192) against its
+    ground truth, and on the parity strip the same PSNR for the HIP render and
+    for the oracle's render of those rays (|dPSNR| is the north_star figure)."""
+    import torch
+    from nerfhip.evaluate import load_packed, psnr, ssim
+    gts, _, _, frames = load_packed(GT_PATH, H, W)
+    vals, ssims = [], []
+    for i, fr in enumerate(frames):
+        pose, K = lego_camera(H, W, i)
+        rgb = pipe.render_image(H, W, pose, K)["rgb_map"].view(H, W, 3).cpu().numpy()
+        vals.append(psnr(rgb, gts[i]))
+        ssims.append(ssim(rgb, gts[i]))
+    torch.cuda.synchronize()
+    out = {"frames": [int(f) for f in frames], "psnr": vals, "psnr_mean": float(np.mean(vals)),
+           "ssim_mean": float(np.mean(ssims)),
+           "metric": "evaluators/nerf.py PSNR (clip to [0,1], -10 log10 mse) and SSIM, "
+                     "mean over the packed test views"}
+    if parity and "_maps" in parity:
+        g, o = parity.pop("_maps")
+        r0, r1 = parity["strip_rows"]
+        gt = gts[0][r0:r1]
+        pg, po = psnr(g, gt), psnr(o, gt)
+        out["strip"] = {"rows": [r0, r1], "frame": int(frames[0]), "psnr_hip": pg,
+                        "psnr_oracle": po, "abs_delta_db": abs(pg - po)}
+    return out
 
 
 def cpu_baseline_c4(pipe, H, W, params, rows):

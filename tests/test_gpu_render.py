@@ -108,7 +108,8 @@ def test_mlp_dense_weights(dev, prec):
 
 
 @pytest.mark.parametrize("gain", [0.05, 8.0])
-def test_mlp_x3_extreme_weight_scales(dev, gain):
+@pytest.mark.parametrize("prec", ["f16x3"])
+def test_mlp_x3_extreme_weight_scales(dev, gain, prec):
     """3-term FP16 split at tiny and at large activations (power-of-two scaling)."""
     from nerfhip.synthetic import make_params
     p = make_params(5, gain, 0.5)
@@ -118,7 +119,7 @@ def test_mlp_x3_extreme_weight_scales(dev, gain):
     rd = rng.normal(size=(n, 3)).astype(np.float32)
     rd /= np.linalg.norm(rd, axis=1, keepdims=True)
     zr = np.sort(rng.uniform(0.5, 3, (n, S)), 1).astype(np.float32)
-    pipe = _pipe(dev, N_samples=S, N_importance=0, mlp_precision="f16x3")
+    pipe = _pipe(dev, N_samples=S, N_importance=0, mlp_precision=prec)
     pipe.set_weights(p)
     raw = pipe.mlp(pipe.coarse, _t(ro, dev), _t(rd, dev), _t(zr, dev), S, n, S)
     pts = (ro[:, None, :] + rd[:, None, :] * zr[:, :, None]).astype(np.float32)

@@ -167,3 +167,21 @@ def test_torch_sum_order(n):
     assert np.array_equal(O.tsum_last(x.numpy()), torch.sum(x, -1).numpy())
     y = torch.rand(129, n, 3, generator=g) ** 3
     assert np.array_equal(O.tsum_dim2(y.numpy()), torch.sum(y, -2).numpy())
+
+
+@pytest.mark.parametrize("name", ["f1_c2_crop", "f2b_c2_dense"])
+def test_torch_cpu_restatement_matches_golden(name):
+    """oracle/torch_render.py (bench.py's timed CPU baseline) renders the golden
+    fixtures like the reference: coarse maps to 1e-5, fine maps through the same
+    per-ray gate as the HIP renderer."""
+    from oracle import torch_render as TR
+    z = load(name)
+    H, W = int(z["H"]), int(z["W"])
+    ro, rd = TR.camera_rays(H, W, z["pose"], z["K"])
+    res = TR.render_rays(ro, rd, params_of(z))
+    n = H * W
+    assert max_err(res["rgb_map_0"], z["out_rgb_map_0"].reshape(n, 3)) < TOL
+    assert max_err(res["acc_map_0"], z["out_acc_map_0"].reshape(n)) < TOL
+    assert rel_err(res["depth_map_0"], z["out_depth_map_0"].reshape(n)) < TOL
+    ok, rep = fine_gate(res, z, load("s_" + name))
+    assert ok, rep

@@ -4,7 +4,8 @@ The fused MLP kernels issue ds_read_b128 through inline asm and wait for them
 explicitly (s_waitcnt lgkmcnt(0)); the compiler believes the destination
 registers are written when the asm issues. This script flags any instruction
 between such a read and its drain that reads or writes one of the pending
-destination VGPRs (a stale read, or a register the late data would clobber).
+destination VGPRs or AGPRs (a stale read, or a register the late data would
+clobber).
 
 The pending set is propagated over the control-flow graph of the .s (basic
 blocks split at labels and branches; successors from s_branch / s_cbranch_* /
@@ -18,12 +19,13 @@ import sys
 
 
 def regs(tok):
-    m = re.match(r"v\[(\d+):(\d+)\]$", tok)
+    """VGPRs and AGPRs named by an operand token, as 'v8' / 'a130' strings."""
+    m = re.match(r"([va])\[(\d+):(\d+)\]$", tok)
     if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
-    m = re.match(r"v(\d+)$", tok)
+        return {f"{m.group(1)}{r}" for r in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r"([va])(\d+)$", tok)
     if m:
-        return {int(m.group(1))}
+        return {f"{m.group(1)}{m.group(2)}"}
     return set()
 
 
