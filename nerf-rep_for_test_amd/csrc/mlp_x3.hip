@@ -90,10 +90,20 @@ constexpr int kX3DmaAhead = MLP_X3_HALF ? 2 : 3;
 #define MLP_X3_LOADER_SPLIT 0
 #endif
 constexpr int kX3Pieces = MLP_X3_LOADERS == 4 ? 8 : 4;   // per loading wave and slice
+// MLP_X3_LOADER_HI: the loading half is waves 4-7 (the second-dispatched half)
+#ifndef MLP_X3_LOADER_HI
+#define MLP_X3_LOADER_HI 0
+#endif
+// MLP_X3_PRIO: s_setprio 1 for waves 4-7 (1) or for waves 0-3 (2) before the
+// tile loop (MI355X_MICROARCH "Two waves per SIMD", item 4)
+#ifndef MLP_X3_PRIO
+#define MLP_X3_PRIO 0
+#endif
 __device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane) {
 #if MLP_X3_LOADERS == 4
   static_assert(MLP_DMA_BUF, "4 loader waves need the buffer-form DMA");
-  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4, kX3Slices);
+  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane,
+                         MLP_X3_LOADER_HI ? wave >= 4 : wave < 4, kX3Slices);
 #else
   static_assert(MLP_DMA_BUF, "the x3 stream (kX3Slices) needs the buffer-form DMA");
   return make_dma_blocks(slices, t, buf, wave * kBlocksPerWave, wave, lane, true, kX3Slices);
@@ -388,6 +398,10 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 
   FragPipe fp;
   fp.late = MLP_X3_HALF ? __builtin_amdgcn_readfirstlane(wave >> 2) : 0;
+#if MLP_X3_PRIO
+  if (__builtin_amdgcn_readfirstlane(wave >> 2) == (MLP_X3_PRIO == 1 ? 1 : 0))
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #if MLP_X3_PERSIST
   const int64_t ntiles = (total + kX3Tile - 1) / kX3Tile;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

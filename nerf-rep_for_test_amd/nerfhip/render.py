@@ -264,9 +264,11 @@ class NerfPipeline:
             if self.enable_ert:       # the counter only drives ESS grid updates
                 self.grid_update_counter = cf + per * total
             return res
-        if p0 % REF_CHUNK:
+        if n > 0 and p0 % REF_CHUNK:
             raise ValueError("with ESS + ERT a band must start on a 2048-ray chunk boundary")
-        c0, c1 = p0 // REF_CHUNK, -(-(p0 + n) // REF_CHUNK)
+        # an empty band (a rank past the last pixel, p0 = H*W) lies after every chunk
+        c0 = p0 // REF_CHUNK if n > 0 else total
+        c1 = -(-(p0 + n) // REF_CHUNK) if n > 0 else total
         upd = [c for c in range(total)
                if any((cf + per * c + k) % self.grid_update_interval == 0 for k in range(per))]
 

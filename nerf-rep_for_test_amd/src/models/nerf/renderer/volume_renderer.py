@@ -264,7 +264,8 @@ class Renderer:
                 disp = np.clip(disp, 0, mx if mx > 0 else 1.0)
                 mx = np.max(disp)
                 rgb8 = (255 * rgb).astype(np.uint8)
-                disp8 = (255 * disp / mx if mx > 0 else disp).astype(np.uint8)
+                with np.errstate(invalid="ignore"):   # NaN disp (acc = 0) casts as the reference's
+                    disp8 = (255 * disp / mx if mx > 0 else disp).astype(np.uint8)
                 rgb8s.append(rgb8)
                 disp8s.append(disp8)
                 if images_dir is not None:

@@ -50,7 +50,13 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_ilv2": ["-DMLP_X3_ILV=2"], "x3_ilv4": ["-DMLP_X3_ILV=4"],
             "x3_persist": ["-DMLP_X3_PERSIST=1"], "x3_pl": ["-DMLP_PERMLANE=1"],
             "x3_persist_pl": ["-DMLP_X3_PERSIST=1", "-DMLP_PERMLANE=1"],
-            "x3_ld4_ilv2": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_ILV=2"]}
+            "x3_ld4_ilv2": ["-DMLP_DMA_BUF=1", "-DMLP_X3_LOADERS=4", "-DMLP_X3_ILV=2"],
+            # static priority for the second-dispatched half / for the loading half
+            "x3_prio_hi": ["-DMLP_X3_PRIO=1"], "x3_prio_lo": ["-DMLP_X3_PRIO=2"],
+            # the loading half = waves 4-7, alone and with priority for waves 0-3
+            "x3_ldhi": ["-DMLP_X3_LOADER_HI=1"],
+            "x3_ldhi_prio_lo": ["-DMLP_X3_LOADER_HI=1", "-DMLP_X3_PRIO=2"],
+            "x3_ilv1": ["-DMLP_X3_ILV=1"], "x3_ilv3": ["-DMLP_X3_ILV=3"]}
 
 
 def is_x3(v):
