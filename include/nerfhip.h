@@ -85,6 +85,34 @@ int nerf_mlp_forward_x3(const float* w_slices, const float* w_head,
                         const float* z, int64_t z_stride, int64_t n, int S,
                         float* raw, nerf_stream_t stream);
 
+/* Training-step compositing (VR:286-357, raw_noise_std 0), differentiable:
+ * forward = the reference's maps for rays [n] with S samples (raw float4
+ * [n*S], z [n][S], rays_d [n][3]) plus the weights and the exclusive
+ * transmittance T [n][S] the backward reads; backward = d raw [n*S] (float4)
+ * and, if d_z is not null, d z [n][S] from the gradients of any of the outputs
+ * (null = zero). Replaces torch autograd's cumprod backward, whose host-side
+ * zero test a HIP graph cannot capture (nerf-rep_for_test_amd/csrc/
+ * train_kernels.hip). */
+int nerf_composite_train_fwd(const float* raw, const float* z, const float* rays_d,
+                             int64_t n, int S, int white, float* rgb, float* disp,
+                             float* acc, float* depth, float* weights, float* trans,
+                             nerf_stream_t stream);
+int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays_d,
+                             const float* weights, const float* trans, const float* acc,
+                             const float* depth, int64_t n, int S, int white,
+                             const float* g_rgb, const float* g_disp, const float* g_acc,
+                             const float* g_depth, const float* g_weights, float* d_raw,
+                             float* d_z, nerf_stream_t stream);
+
+/* Backward of _sample_fine with training-mode u (VR:239-268) + the merge
+ * torch.sort(cat(z, z_fine)) (VR:181-184) whose forward is nerf_sample_fine:
+ * d_weights [n][S] (rows 0 and S-1 zero) from g_zall [n][S + n_imp]. z [n][S],
+ * weights [n][S], u [n][n_imp] as given to the forward. S <= 130,
+ * n_imp <= 256. */
+int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
+                        const float* g_zall, int64_t n, int S, int n_imp,
+                        float* d_weights, nerf_stream_t stream);
+
 /* Training MLP (BASELINE configs[2]): the 8x256 NeRF MLP of a training step
  * (network.py:49-74 forward and its autograd backward) as layer GEMMs over
  * feature-major activations ([F][P]: row f = feature f of every sample),

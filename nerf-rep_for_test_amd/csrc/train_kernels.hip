@@ -1,0 +1,342 @@
+// Training-step kernels around the MLPs (BASELINE configs[2]):
+// the differentiable compositing of _raw2outputs (VR:286-357) and importance
+// sampling of _sample_fine (VR:239-268, training-mode u) + the sorted merge of
+// VR:181-184, forward and backward, so the whole step runs on hand-written
+// kernels without data-dependent host syncs (torch's cumprod backward tests its
+// input for zeros on the host, which a HIP graph cannot capture).
+//
+// Compositing: one thread per ray (a training batch is ~1e3 rays x 64-192
+// samples); the transmittance is the reference's exclusive cumprod of
+// (1 - a + 1e-10) accumulated in double like torch's CPU kernel, the map sums
+// in torch's CPU summation orders (common.h tsum_last / tsum_dim2).
+// The forward also stores T (the backward reads it instead of dividing w by a).
+// Backward, with G_i = dL/dw_i + g_rgb . c_i + g_acc' + g_depth' z_i the total
+// gradient reaching weight i (white background folds -sum(g_rgb) into g_acc'):
+//   dL/da_i = T_i (G_i - B_i),  B_i = sum_{j>i} G_j a_j prod_{i<k<j} x_k,
+//   x_k = 1 - a_k + 1e-10, B by the reverse recurrence B_i = G_{i+1} a_{i+1} +
+//   x_{i+1} B_{i+1} (no division: zero-safe), then a = 1 - exp(-relu(r) d).
+//
+// Importance sampling: one wave per ray (LDS rows as the inference
+// sample_fine kernel), forward = nerf_sample_fine; the backward recomputes the
+// cdf and each fine sample's bin, locates the sample in the merged row, and
+// takes dL/dz_all there back to dL/dweights through t = (u - c0)/(c1 - c0),
+// the cdf (reverse cumsum) and the normalisation pdf = w'/sum(w').
+#include "common.h"
+
+namespace nerfhip {
+
+// ---------------------------------------------------------------------------
+// compositing
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void composite_train_fwd_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rays_d,
+    int64_t n, int S, int white, float* __restrict__ rgb, float* __restrict__ disp,
+    float* __restrict__ acc, float* __restrict__ depth, float* __restrict__ w,
+    float* __restrict__ trans) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const float4* rr = raw + r * S;
+  const float* zr = z + r * S;
+  float* wr = w + r * S;
+  float* tr = trans + r * S;
+  const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
+  double carry = 1.0;
+  for (int s = 0; s < S; ++s) {
+    const float zs = zr[s];
+    const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;     // VR:290-292
+    const float a = 1.0f - expf((-fmaxf(rr[s].w, 0.0f)) * dist);          // VR:288
+    const float T = (float)carry;
+    tr[s] = T;
+    wr[s] = a * T;                                                         // VR:329
+    carry = carry * (double)((1.0f - a) + 1e-10f);
+  }
+  float m[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    m[c] = tsum_dim2(S, [&](int s) {
+      const float4 v = rr[s];
+      return wr[s] * sigm(c == 0 ? v.x : (c == 1 ? v.y : v.z));
+    });
+  const float dp = tsum_last(S, [&](int s) { return wr[s] * zr[s]; });
+  const float ac = tsum_last(S, [&](int s) { return wr[s]; });
+  disp[r] = 1.0f / torch_max(1e-10f, dp / ac);
+  acc[r] = ac;
+  depth[r] = dp;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) rgb[r * 3 + c] = white ? m[c] + (1.0f - ac) : m[c];
+}
+
+// Gradients: g_rgb [n,3], g_disp / g_acc / g_depth [n], g_w [n,S] (any may be
+// null = zero). Outputs d_raw [n,S,4] and d_z [n,S] (null: not needed).
+__global__ __launch_bounds__(256) void composite_train_bwd_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rays_d,
+    const float* __restrict__ w, const float* __restrict__ trans, const float* __restrict__ acc,
+    const float* __restrict__ depth,
+    int64_t n, int S, int white, const float* __restrict__ g_rgb,
+    const float* __restrict__ g_disp, const float* __restrict__ g_acc,
+    const float* __restrict__ g_depth, const float* __restrict__ g_w, float4* __restrict__ d_raw,
+    float* __restrict__ d_z) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const float4* rr = raw + r * S;
+  const float* zr = z + r * S;
+  const float* wr = w + r * S;
+  const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
+  float gr[3] = {0.f, 0.f, 0.f};
+  if (g_rgb) for (int c = 0; c < 3; ++c) gr[c] = g_rgb[r * 3 + c];
+  float ga = g_acc ? g_acc[r] : 0.0f;
+  float gd = g_depth ? g_depth[r] : 0.0f;
+  if (white) ga -= (gr[0] + gr[1]) + gr[2];          // rgb_map += 1 - acc (VR:353-354)
+  if (g_disp) {   // disp = 1 / max(1e-10, depth / acc): through depth / acc where > 1e-10
+    const float ac = acc[r], dp = depth[r], q = dp / ac;
+    if (q > 1e-10f) {
+      const float gq = -g_disp[r] / (q * q);
+      gd += gq / ac;
+      ga -= gq * dp / (ac * ac);
+    }
+  }
+  float* dzr = d_z ? d_z + r * S : nullptr;
+  if (dzr) for (int s = 0; s < S; ++s) dzr[s] = 0.0f;
+  // reverse sweep: B_s = sum_{j>s} G_j a_j prod_{s<k<j} x_k
+  float B = 0.0f;
+  for (int s = S - 1; s >= 0; --s) {
+    const float4 v = rr[s];
+    const float zs = zr[s];
+    const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;
+    const float sig = fmaxf(v.w, 0.0f);
+    const float e = expf(-sig * dist);
+    const float a = 1.0f - e;
+    const float ws = wr[s];
+    const float c0 = sigm(v.x), c1 = sigm(v.y), c2 = sigm(v.z);
+    const float G = (g_w ? g_w[r * S + s] : 0.0f) + gr[0] * c0 + gr[1] * c1 + gr[2] * c2 + ga +
+                    gd * zs;
+    const float T = trans[r * S + s];
+    const float ga_s = T * (G - B);                     // dL/da_s
+    // a = 1 - exp(-relu(r3) d): da/dr3 = d e (r3 > 0), da/dd = relu(r3) e
+    const float g_sig = v.w > 0.0f ? ga_s * dist * e : 0.0f;
+    float4 dr;
+    dr.x = ws * gr[0] * c0 * (1.0f - c0);
+    dr.y = ws * gr[1] * c1 * (1.0f - c1);
+    dr.z = ws * gr[2] * c2 * (1.0f - c2);
+    dr.w = g_sig;
+    d_raw[r * S + s] = dr;
+    if (dzr) {
+      dzr[s] += ws * gd;                                  // depth = sum w z
+      if (s < S - 1) {
+        const float g_dist = ga_s * sig * e * nd;         // dist = (z[s+1] - z[s]) |d|
+        dzr[s + 1] += g_dist;
+        dzr[s] -= g_dist;
+      }
+    }
+    B = G * a + ((1.0f - a) + 1e-10f) * B;               // B_{s-1}
+  }
+}
+
+// ---------------------------------------------------------------------------
+// importance sampling backward (forward: nerf_sample_fine)
+// ---------------------------------------------------------------------------
+constexpr int PDF_WAVES = 4;
+constexpr int PDF_MAX_S = 130;
+constexpr int PDF_MAX_IMP = 256;
+constexpr int PDF_ROW = PDF_MAX_S + 2;
+
+struct PdfLds {
+  float zc[PDF_ROW];
+  float wv[PDF_ROW];
+  float cdf[PDF_ROW];
+  float bins[PDF_ROW];
+  float zf[PDF_MAX_IMP];      // fine samples (u order)
+  float gt[PDF_MAX_IMP];      // dL/dt_j
+  float dc0[PDF_MAX_IMP];     // dt_j/dc[below_j]
+  float dc1[PDF_MAX_IMP];     // dt_j/dc[above_j]
+  short lo[PDF_MAX_IMP], hi[PDF_MAX_IMP];
+  float gcdf[PDF_ROW];
+  float gpdf[PDF_ROW];
+};
+
+__device__ __forceinline__ float wave_tsum_last_pdf(const float* v, int n, int lane) {
+  if (n < 8) return tsum_last(n, [&](int i) { return v[i]; });
+  const int nv = n >> 3, nilp = nv >> 2, l = lane & 7;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int ii = 0; ii < nilp; ++ii) {
+    const int b = ii * 32 + l;
+    a0 = a0 + v[b];
+    a1 = a1 + v[b + 8];
+    a2 = a2 + v[b + 16];
+    a3 = a3 + v[b + 24];
+  }
+  for (int q = nilp * 4; q < nv; ++q) a0 = a0 + v[q * 8 + l];
+  const float part = ((a0 + a1) + a2) + a3;
+  float fin = 0.f;
+  for (int k = nv * 8; k < n; ++k) fin = fin + v[k];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) fin = fin + __shfl(part, q);
+  return fin;
+}
+
+__device__ __forceinline__ double wave_sum_scan_d(double p, int lane) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const double q = __shfl_up(p, o);
+    if (lane >= o) p += q;
+  }
+  return p;
+}
+
+__device__ __forceinline__ int ub(const float* a, int n, float x) {   // # a[i] <= x
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// d_w [n, S] = dL/dweights of the coarse pass given g_zall [n, S + n_imp]
+// (dL/d z_all). z [n, S] coarse depths (per-ray rows), weights [n, S], u [n, n_imp].
+__global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
+    const float* __restrict__ z, const float* __restrict__ weights, const float* __restrict__ u,
+    const float* __restrict__ g_zall, int64_t n, int S, int n_imp, float* __restrict__ d_w) {
+  __shared__ PdfLds sm[PDF_WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t ray = (int64_t)blockIdx.x * PDF_WAVES + wave;
+  if (ray >= n) return;   // wave-uniform; no block barriers below
+  PdfLds& L = sm[wave];
+  const float* zr = z + ray * S;
+  const float* wr = weights + ray * S;
+  const float* ur = u + ray * n_imp;
+  const float* gz = g_zall + ray * (int64_t)(S + n_imp);
+  const int nb = S - 1, nw = S - 2;
+  for (int s = lane; s < S; s += 64) L.zc[s] = zr[s];
+  for (int s = lane; s < nw; s += 64) L.wv[s] = wr[s + 1] + 1e-5f;
+  __builtin_amdgcn_wave_barrier();
+  for (int s = lane; s < nb; s += 64) L.bins[s] = 0.5f * (L.zc[s + 1] + L.zc[s]);
+  const float tot = wave_tsum_last_pdf(L.wv, nw, lane);
+  double carry = 0.0;
+  if (lane == 0) L.cdf[0] = 0.0f;
+  for (int b = 0; b < nw; b += 64) {
+    const int s = b + lane;
+    const double pdf = s < nw ? (double)(L.wv[s] / tot) : 0.0;
+    const double inc = carry + wave_sum_scan_d(pdf, lane);
+    if (s < nw) L.cdf[s + 1] = (float)inc;
+    carry = __shfl(inc, 63);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // recompute each fine sample and the derivatives of its t
+  for (int j = lane; j < n_imp; j += 64) {
+    const float uj = ur[j];
+    const int inds = ub(L.cdf, nb, uj);
+    const int below = inds - 1 > 0 ? inds - 1 : 0;
+    const int above = inds < nb - 1 ? inds : nb - 1;
+    const float c0 = L.cdf[below], c1 = L.cdf[above];
+    const float b0 = L.bins[below], b1 = L.bins[above];
+    const float D = c1 - c0;
+    const bool clamped = D < 1e-5f;
+    const float den = clamped ? 1.0f : D;
+    const float t = (uj - c0) / den;
+    L.zf[j] = b0 + t * (b1 - b0);
+    L.lo[j] = (short)below;
+    L.hi[j] = (short)above;
+    L.dc0[j] = clamped ? -1.0f : (t - 1.0f) / den;
+    L.dc1[j] = clamped ? 0.0f : -t / den;
+    L.gt[j] = b1 - b0;   // times dL/dz_f, below
+  }
+  __builtin_amdgcn_wave_barrier();
+  // position of fine sample j in the merged row: its rank among the fine samples
+  // (ties in u order) + the coarse depths <= it (torch.sort of cat(z, z_f))
+  for (int j = lane; j < n_imp; j += 64) {
+    const float x = L.zf[j];
+    int rank = 0;
+    for (int k = 0; k < n_imp; ++k) {
+      const float y = L.zf[k];
+      rank += (y < x) || (y == x && k < j);
+    }
+    const int pos = rank + ub(L.zc, S, x);
+    L.gt[j] = L.gt[j] * gz[pos];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // dL/dcdf[k], summed in sample order (deterministic)
+  for (int k = lane; k < nb; k += 64) {
+    float acc = 0.0f;
+    for (int j = 0; j < n_imp; ++j) {
+      if (L.lo[j] == k) acc += L.gt[j] * L.dc0[j];
+      if (L.hi[j] == k) acc += L.gt[j] * L.dc1[j];
+    }
+    L.gcdf[k] = acc;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // cdf[k] = sum_{i<k} pdf[i]: dL/dpdf[i] = sum_{k>i} dL/dcdf[k] (reverse cumsum)
+  double rc = 0.0;
+  for (int b = ((nw - 1) / 64) * 64; b >= 0; b -= 64) {
+    const int i = b + lane;
+    const double v = (i < nw) ? (double)L.gcdf[i + 1] : 0.0;
+    // suffix sum within the block: reverse the lane order for an inclusive scan
+    const double rv = __shfl(v, 63 - lane);
+    const double sc = wave_sum_scan_d(rv, lane);
+    const double suf = __shfl(sc, 63 - lane) + rc;
+    if (i < nw) L.gpdf[i] = (float)suf;
+    rc = rc + __shfl(sc, 63);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // pdf = w' / tot: dL/dw'_i = (gpdf_i - sum_m gpdf_m w'_m / tot) / tot
+  float part = 0.0f;
+  for (int i = lane; i < nw; i += 64) part += L.gpdf[i] * L.wv[i];
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  const float mean = part / tot;
+  float* dw = d_w + ray * S;
+  for (int s = lane; s < S; s += 64) {
+    const int i = s - 1;
+    dw[s] = (i >= 0 && i < nw) ? (L.gpdf[i] - mean) / tot : 0.0f;
+  }
+}
+
+extern "C" {
+
+int nerf_composite_train_fwd(const float* raw, const float* z, const float* rays_d, int64_t n,
+                             int S, int white, float* rgb, float* disp, float* acc, float* depth,
+                             float* weights, float* trans, nerf_stream_t stream) {
+  NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth && weights && trans,
+               "nerf_composite_train_fwd: null pointer");
+  NERF_REQUIRE(n >= 0 && S >= 1 && S < 1024, "nerf_composite_train_fwd: bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(composite_train_fwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), (const float4*)raw, z, rays_d, n, S, white, rgb, disp,
+                     acc, depth, weights, trans);
+  return check_launch("composite_train_fwd_kernel");
+}
+
+int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays_d,
+                             const float* weights, const float* trans, const float* acc,
+                             const float* depth,
+                             int64_t n, int S, int white, const float* g_rgb, const float* g_disp,
+                             const float* g_acc, const float* g_depth, const float* g_weights,
+                             float* d_raw, float* d_z, nerf_stream_t stream) {
+  NERF_REQUIRE(raw && z && rays_d && weights && trans && acc && depth && d_raw,
+               "nerf_composite_train_bwd: null pointer");
+  NERF_REQUIRE(n >= 0 && S >= 1 && S < 1024, "nerf_composite_train_bwd: bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(composite_train_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), (const float4*)raw, z, rays_d, weights, trans, acc, depth,
+                     n, S,
+                     white, g_rgb, g_disp, g_acc, g_depth, g_weights, (float4*)d_raw, d_z);
+  return check_launch("composite_train_bwd_kernel");
+}
+
+int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
+                        const float* g_zall, int64_t n, int S, int n_imp, float* d_weights,
+                        nerf_stream_t stream) {
+  NERF_REQUIRE(z && weights && u && g_zall && d_weights, "nerf_sample_pdf_bwd: null pointer");
+  NERF_REQUIRE(n >= 0 && S >= 3 && S <= PDF_MAX_S && n_imp >= 1 && n_imp <= PDF_MAX_IMP,
+               "nerf_sample_pdf_bwd: bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sample_pdf_bwd_kernel, dim3((unsigned)cdiv(n, PDF_WAVES)),
+                     dim3(64 * PDF_WAVES), 0, as_stream(stream), z, weights, u, g_zall, n, S,
+                     n_imp, d_weights);
+  return check_launch("sample_pdf_bwd_kernel");
+}
+
+}  // extern "C"
+
+}  // namespace nerfhip

@@ -30,6 +30,10 @@ SIGNATURES = {
                            _P, _S]),
     "nerf_x3_wgrad": (_I, [_P, _I64, _I, _P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _S]),
     "nerf_x3_pack": (_I, [_P, _I, _S]),
+    "nerf_composite_train_fwd": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _S]),
+    "nerf_composite_train_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _P, _P, _P, _P,
+                                      _P, _P, _P, _S]),
+    "nerf_sample_pdf_bwd": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _S]),
     "nerf_freq_encode_fm": (_I, [_P, _I64, _I64, _I, _P, _I64, _P, _S]),
     "nerf_freq_encode_fm_backward": (_I, [_P, _I64, _P, _I64, _I64, _I, _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),

@@ -116,7 +116,8 @@ def composite_ert(raw, z, rays_d, thr, white_bkgd, chunk=2048):
 
 
 def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query,
-                 detach_fine_samples=False, composite_fn=None, on_composite=None):
+                 detach_fine_samples=False, composite_fn=None, on_composite=None,
+                 hip_ops=False):
     """The differentiable part of a training step (VR:164-194): coarse depths z
     [n, S] (no gradient) -> coarse maps, importance samples from the coarse
     weights (u [n, N_importance]), fine maps. fine=None: coarse only.
@@ -127,7 +128,14 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
     the original NeRF does (tf.stop_gradient on z_samples).
     composite_fn(raw, z, rays_d) -> (rgb, disp, acc, weights, depth) replaces
     _raw2outputs (e.g. composite_ert); on_composite(kind, z, raw, weights) is
-    called after each composite (kind 0 coarse, 1 fine: the ESS grid hook)."""
+    called after each composite (kind 0 coarse, 1 fine: the ESS grid hook).
+    hip_ops: compositing (unless composite_fn is given) and importance sampling
+    + merge on the HIP kernels of train_ops (no host syncs: graph-capturable)."""
+    if composite_fn is None and hip_ops:
+        from .train_ops import composite_hip
+
+        def composite_fn(raw, zz, rd):
+            return composite_hip(raw, zz, rd, white_bkgd)
     if composite_fn is None:
         def composite_fn(raw, zz, rd):
             return composite(raw, zz, rd, white_bkgd)
@@ -138,11 +146,15 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
         on_composite(0, z, raw, w)
     out = {"rgb_map_0": rgb0, "disp_map_0": disp0, "acc_map_0": acc0, "depth_map_0": depth0}
     if fine is not None:
-        mids = 0.5 * (z[..., 1:] + z[..., :-1])
-        zf = sample_pdf(mids, w[..., 1:-1], u)
-        if detach_fine_samples:
-            zf = zf.detach()
-        z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
+        if hip_ops:
+            from .train_ops import sample_fine_hip
+            z2 = sample_fine_hip(w.detach() if detach_fine_samples else w, z, u)
+        else:
+            mids = 0.5 * (z[..., 1:] + z[..., :-1])
+            zf = sample_pdf(mids, w[..., 1:-1], u)
+            if detach_fine_samples:
+                zf = zf.detach()
+            z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
         pts2 = rays_o[:, None, :] + rays_d[:, None, :] * z2[..., None]
         raw2 = query_fn(fine, pts2, rays_d)
         rgb, disp, acc, w2, depth = composite_fn(raw2, z2, rays_d)
@@ -210,7 +222,8 @@ def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
             def comp(raw, zz, rdd):
                 return composite(raw, zz, rdd, pipe.white_bkgd)
         outs.append(render_train(coarse, fine if NI > 0 else None, ro, rd, z, u,
-                                 pipe.white_bkgd, query_fn, detach_fine_samples, comp, hook))
+                                 pipe.white_bkgd, query_fn, detach_fine_samples,
+                                 comp if pipe.enable_ert else None, hook, hip_ops=True))
         if pipe.enable_ert:
             pipe.grid_update_counter = counter0 + pipe._calls_per_chunk() * -(-m // REF_CHUNK)
         p += m
@@ -232,7 +245,7 @@ class NerfTrainer:
 
     def __init__(self, device, params, N_samples=64, N_importance=128, near=2.0, far=6.0,
                  white_bkgd=True, lr=5e-4, clip_value=40.0, mlp="x3",
-                 detach_fine_samples=False):
+                 detach_fine_samples=False, graph=False, ops="hip"):
         from src.models.nerf.network import NeRF
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -248,7 +261,25 @@ class NerfTrainer:
         self.coarse = NeRF().to(self.device)
         self.fine = NeRF().to(self.device)
         self.load(params)
-        self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0)
+        # graph=True: the whole step (both MLPs forward + backward, compositing,
+        # sampling, loss, clip, Adam) is captured once per batch shape into a HIP
+        # graph and replayed: one launch instead of several hundred. Adam then
+        # keeps its step count and learning rate on the device (capturable,
+        # lr tensor: set_lr updates it in place).
+        if ops not in ("hip", "torch"):
+            raise ValueError("ops must be 'hip' or 'torch'")
+        if graph and ops != "hip":
+            raise ValueError("graph=True needs ops='hip' (torch's cumprod backward syncs)")
+        self.ops = ops
+        self.graph = bool(graph)
+        if self.graph:
+            self.opt = torch.optim.Adam(self.parameters(),
+                                        lr=torch.tensor(lr, device=self.device), eps=1e-8,
+                                        weight_decay=0.0, capturable=True, foreach=True)
+        else:
+            self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0)
+        self._graphs = {}
+        self._warm = {}
         self.z_base = coarse_depth_table(near, far, self.N_samples, False).to(self.device)
 
     def parameters(self):
@@ -278,15 +309,53 @@ class NerfTrainer:
         from .train_mlp import query_x3
         return render_train(self.coarse, self.fine if self.N_importance > 0 else None,
                             rays_o, rays_d, z, u, self.white_bkgd,
-                            query_x3 if self.mlp == "x3" else query, self.detach_fine_samples)
+                            query_x3 if self.mlp == "x3" else query, self.detach_fine_samples,
+                            hip_ops=self.ops == "hip")
 
     def loss(self, out, target):
         return mse_losses(out, target)
 
+    def set_lr(self, lr):
+        for g in self.opt.param_groups:
+            if torch.is_tensor(g["lr"]):
+                g["lr"].fill_(lr)
+            else:
+                g["lr"] = lr
+
     def step(self, rays_o, rays_d, target, t_rand=None, u=None, group=None):
         """One optimisation step; returns the loss dict (device tensors). With a
         process group, each rank's gradients are averaged (data parallel: one
-        flat bucket, one all-reduce over RCCL) before clipping and Adam."""
+        flat bucket, one all-reduce over RCCL) before clipping and Adam.
+        In graph mode (no explicit draws given) the first two steps of a batch
+        shape run eagerly (they create the packers' buffers, Adam's state and
+        the BLAS handles), the third is captured and every step from then on
+        replays the graph with the batch copied into its static inputs; the
+        returned losses are the graph's output tensors."""
+        if self.graph and t_rand is None and u is None:
+            return self._step_graphed(rays_o, rays_d, target, group)
+        return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
+
+    def _step_graphed(self, rays_o, rays_d, target, group):
+        key = (rays_o.shape[0], group is not None)
+        g = self._graphs.get(key)
+        if g is None:
+            if self._warm.get(key, 0) < 2:
+                self._warm[key] = self._warm.get(key, 0) + 1
+                return self._step_eager(rays_o, rays_d, target, None, None, group)
+            static = (rays_o.detach().clone(), rays_d.detach().clone(), target.detach().clone())
+            graph = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(graph):
+                out = self._step_eager(*static, None, None, group)
+            g = self._graphs[key] = (graph, static, out)
+        graph, (s_ro, s_rd, s_t), out = g
+        s_ro.copy_(rays_o)
+        s_rd.copy_(rays_d)
+        s_t.copy_(target)
+        graph.replay()
+        return out
+
+    def _step_eager(self, rays_o, rays_d, target, t_rand=None, u=None, group=None):
         n = rays_o.shape[0]
         if t_rand is None:
             t_rand = torch.rand((n, self.N_samples), device=self.device)

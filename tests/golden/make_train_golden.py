@@ -49,7 +49,10 @@ def main():
         capture(name, spec, cfg, Network, vr, meta)
 
 
-def capture(name, SPEC, cfg, Network, vr, meta):
+def capture(name, SPEC, cfg, Network, vr, meta, params=None, write=True):
+    """One reference training step; writes tests/golden/<name>.npz (write=True)
+    and returns the record. params overrides the spec's generated weights
+    (make_train_sensitivity.py: exact reparametrisations)."""
     import torch
     frames, angle = meta["frames"], float(meta["camera_angle_x"])
     cfg.task_arg.N_importance = 128
@@ -59,7 +62,8 @@ def capture(name, SPEC, cfg, Network, vr, meta):
     cfg.enable_ert = bool(SPEC.get("ess_ert", False))
     cfg.ert_threshold = 0.01
     seed, gain, ab = SPEC["w"]
-    params = mg.make_params(seed, gain, ab)
+    if params is None:
+        params = mg.make_params(seed, gain, ab)
     net = Network()
     mg.load_into_network(net, params)
     net.train()
@@ -132,9 +136,12 @@ def capture(name, SPEC, cfg, Network, vr, meta):
             rec["gcnorm__" + k] = np.float64(coarse_only[k].norm().item())
             rec["gchead__" + k] = coarse_only[k].numpy().reshape(-1)[:64].copy()
     rec["param_names"] = np.array(names)
+    if not write:
+        return rec
     path = os.path.join(HERE, name + ".npz")
     np.savez_compressed(path, **rec)
     print("wrote", path, "loss", loss.item(), "params", len(names))
+    return rec
 
 
 if __name__ == "__main__":

@@ -4,9 +4,12 @@ backward (tests/golden/t1_train_step.npz, captured by make_train_golden.py).
 Tolerances: the coarse pass is deterministic up to FP32 GEMM order (1e-5 on
 rgb); the fine samples are a searchsorted of the coarse weights, so the fine
 rgb is compared by PSNR; the gradients of the coarse loss alone to 1e-3, those
-of the full loss by relative norm to 5 % (the fine loss reaches the coarse
-network through the sample positions, where sin(2^9 x) amplifies FP32
-GEMM-order differences; measured worst case 3.7 %, the coarse density bias).
+of the full loss by relative norm to max(2e-3, 2 x the reference's own spread
+for that tensor) (tests/golden/ts_*.npz, make_train_sensitivity.py: the fine
+loss reaches the coarse network through the sample positions, where sin(2^9 x)
+and 1/(cdf[above] - cdf[below]) amplify float32 rounding; the reference itself
+moves the coarse density bias's norm by 7.5 % under an exact reparametrisation
+of its network, most other tensors by < 0.1 %).
 The same math on the CPU matches the reference to 1e-5 (tests/test_train.py).
 Both MLP back ends are held to the same bounds: the x3 MFMA kernels
 (train_mlp.py, the default) and torch modules on hipBLASLt FP32 GEMMs."""
@@ -26,21 +29,28 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _setup(dev, mlp="x3"):
+def _full_loss_tol(name, k):
+    """Per-tensor bound on the full-loss gradient norm: the reference's own spread."""
+    ts = load("ts_" + name)
+    return max(2e-3, 2.0 * float(ts["gnorm_spread__" + k]))
+
+
+def _setup(dev, mlp="x3", ops="hip"):
     from nerfhip.render import NerfPipeline
     from nerfhip.train import NerfTrainer
     z = load("t1_train_step")
     params = params_of(z)
-    tr = NerfTrainer(dev, params, mlp=mlp)
+    tr = NerfTrainer(dev, params, mlp=mlp, ops=ops)
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128)
     ro, rd = pipe.camera_rays(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
     return z, tr, ro, rd, t(z["t_rand"]), t(z["u"]), t(z["gt"].reshape(-1, 3))
 
 
-@pytest.mark.parametrize("mlp", ["x3", "torch"])
-def test_forward_loss_and_gradients_match_reference(dev, mlp):
-    z, tr, ro, rd, t_rand, u, gt = _setup(dev, mlp)
+@pytest.mark.parametrize("mlp,ops", [("x3", "hip"), ("torch", "hip"), ("x3", "torch"),
+                                     ("torch", "torch")])
+def test_forward_loss_and_gradients_match_reference(dev, mlp, ops):
+    z, tr, ro, rd, t_rand, u, gt = _setup(dev, mlp, ops)
     out = tr.forward(ro, rd, t_rand, u)
     assert max_err(out["rgb_map_0"].detach().cpu().numpy(), z["rgb_map_0"]) < 1e-5
     assert psnr(out["rgb_map"].detach().cpu().numpy(), z["rgb_map"]) > 60.0
@@ -66,7 +76,8 @@ def test_forward_loss_and_gradients_match_reference(dev, mlp):
     assert sorted(names) == sorted(grads)
     for k in names:
         ref_norm = float(z["gnorm__" + k])
-        assert abs(grads[k].norm().item() - ref_norm) <= 5e-2 * ref_norm + 1e-9, k
+        assert abs(grads[k].norm().item() - ref_norm) <= \
+            _full_loss_tol("t1_train_step", k) * ref_norm + 1e-9, k
 
 
 @pytest.mark.parametrize("mlp", ["x3", "torch"])
@@ -132,7 +143,8 @@ def _plugin_train_render(dev, name, mlp):
 def test_plugin_training_render_matches_reference(dev, name, mlp):
     """North_star drop-in for train.py: the plugin's training-mode render gives the
     reference's coarse maps (1e-5), losses and gradients (coarse loss alone 1e-3
-    of each tensor's norm; full loss: norms within 5 %, as the trainer test),
+    of each tensor's norm; full loss: norms within the reference's own spread,
+    as the trainer test),
     with ERT/ESS (t2) also the grid self-update and call counter exactly."""
     from goldlib import rel_err
     z, net, rend, out = _plugin_train_render(dev, name, mlp)
@@ -174,7 +186,7 @@ def test_plugin_training_render_matches_reference(dev, name, mlp):
     for k in [str(s) for s in z["param_names"]]:
         ref_norm = float(z["gnorm__" + k])
         assert abs(params[k].grad.detach().double().norm().item() - ref_norm) <= \
-            5e-2 * ref_norm + 1e-9, k
+            _full_loss_tol(name, k) * ref_norm + 1e-9, k
 
 
 def test_plugin_novel_view_sequence(dev, tmp_path):
@@ -209,3 +221,26 @@ def test_plugin_novel_view_sequence(dev, tmp_path):
     ref = (255 * np.clip(one["rgb_map"].cpu().numpy(), 0, 1)).astype(np.uint8)
     np.testing.assert_array_equal(rgb8[2], ref)
     reset()
+
+
+@pytest.mark.parametrize("mlp", ["x3", "torch"])
+def test_graph_step_trains_and_honours_lr(dev, mlp):
+    """graph=True: eager warm-up steps, then one captured HIP graph replayed per
+    step (static inputs refreshed from each batch); the loss falls like the eager
+    trainer's, the device-side learning rate is honoured (lr 0 leaves every
+    parameter bitwise unchanged), clip_grad_value_(40) holds."""
+    from nerfhip.train import NerfTrainer
+    z, _, ro, rd, _, _, gt = _setup(dev, mlp)
+    tr = NerfTrainer(dev, params_of(z), mlp=mlp, graph=True)
+    first = tr.step(ro, rd, gt)["loss"].item()
+    for _ in range(30):
+        last = tr.step(ro, rd, gt)["loss"].item()
+    assert len(tr._graphs) == 1
+    assert np.isfinite(last) and last < 0.8 * first
+    for p in tr.parameters():
+        assert p.grad is not None and p.grad.abs().max() <= 40.0
+    tr.set_lr(0.0)
+    before = [p.detach().clone() for p in tr.parameters()]
+    tr.step(ro[::-1].contiguous(), rd[::-1].contiguous(), gt)
+    for a, b in zip(before, tr.parameters()):
+        assert torch.equal(a, b)

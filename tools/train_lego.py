@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--detach-fine-samples", action="store_true",
                     help="stop the fine loss's gradient at the importance samples (original "
                          "NeRF); the reference lets it reach the coarse network")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a HIP graph")
     ap.add_argument("--check-finite", action="store_true",
                     help="stop at the first step whose loss or parameters are not finite")
     args = ap.parse_args()
@@ -89,7 +90,8 @@ def main():
     for prefix in ("model", "model_fine"):          # nn.Linear default initialisation
         for k, v in NeRF().state_dict().items():
             init[f"{prefix}.{k}"] = v
-    tr = NerfTrainer(dev, init, mlp=args.mlp, detach_fine_samples=args.detach_fine_samples)
+    tr = NerfTrainer(dev, init, mlp=args.mlp, detach_fine_samples=args.detach_fine_samples,
+                     graph=args.graph)
     step0 = 0
     if args.resume:
         ck = load_checkpoint(args.resume)
@@ -128,8 +130,7 @@ def main():
     last = (t0, step)
     log = []
     while step < args.steps and time.perf_counter() - t_start < args.max_seconds:
-        for g in tr.opt.param_groups:
-            g["lr"] = args.lr * math.exp(gamma * step)
+        tr.set_lr(args.lr * math.exp(gamma * step))
         losses = tr.step(*batch(step))
         step += 1
         if args.check_finite:
