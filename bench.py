@@ -90,6 +90,10 @@ def main():
     ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
                     help="c3: the MLPs on the x3 MFMA training kernels (default) or as torch "
                          "modules (FP32 hipBLASLt GEMMs)")
+    ap.add_argument("--train-graph", action="store_true",
+                    help="c3: replay the step as one HIP graph (capturable Adam) instead of "
+                         "launching it op by op; the step is GPU-bound (~7 ms of kernel time), "
+                         "the graph measured 0.4 ms slower")
     ap.add_argument("--no-fp32-run", action="store_true",
                     help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
     args = ap.parse_args()
@@ -157,6 +161,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         pipe.timer = []
+        pipe.ert_stats = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
@@ -196,6 +201,15 @@ def main():
                    "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
         "roofline": roof,
     }
+    if c4:
+        ev, full = pipe.evaluated_samples()
+        result["ert_compaction"] = {
+            "evaluated_samples_per_ray": ev / (rays / world),
+            "full_samples_per_ray": full / (rays / world),
+            "evaluated_fraction": ev / max(1, full),
+            "note": "MLP samples evaluated per ray (coarse 64 + fine 192 in full) with depth "
+                    "segments of 32 and rays retired at T < 0.01 (their later weights are "
+                    "zeroed by _raw2outputs_with_ert, VR:1115-1123)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if c4:
             result["cpu_baseline"], result["parity"] = cpu_baseline_c4(
@@ -242,7 +256,8 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
     poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
     K = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32,
                      device=dev)
-    tr = NerfTrainer(dev, params, mlp=args.train_mlp)
+    graph = args.train_graph
+    tr = NerfTrainer(dev, params, mlp=args.train_mlp, graph=graph)
     group = dist.group.WORLD if world > 1 else None
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     nrays = 1024
@@ -285,6 +300,8 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
                                "rank, perturb 1, training-mode u, MSE coarse+fine, clip 40, Adam",
                    "baseline_config": "configs[2]", "N_rays": nrays, "N_samples": 64,
                    "N_importance": 128, "train_mlp": args.train_mlp,
+                   "step_launch": "one HIP graph replay per step (captured on the 3rd step)"
+                                  if graph else "eager (op-by-op launches)",
                    "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
         "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
@@ -325,9 +342,12 @@ def roofline(precision, timer, elapsed, world, H, W):
     recorded on the stream it is launched on."""
     from nerfhip.render import NerfPipeline
     mlp_ms = sum(a.elapsed_time(b) for a, b, _, _ in timer)
-    mlp_samples = sum(s for _, _, s, _ in timer)
+    # ERT-compacted launches record their device-side sample count (resolved here,
+    # after the timed region) and no byte figure
+    mlp_samples = sum(int(s) for _, _, s, _ in timer)
     n_launch = len(timer)
-    mlp_bytes = sum(b for _, _, _, b in timer)   # NerfPipeline.mlp_bytes per launch
+    mlp_bytes = sum(b if b is not None else int(s) * 16 + NerfPipeline.MLP_WEIGHT_BYTES
+                    for _, _, s, b in timer)
     flops = mlp_samples * NerfPipeline.MLP_FLOP_PER_SAMPLE
     algo_tflops = flops / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     if precision == "fp32":

@@ -113,6 +113,24 @@ int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
                         const float* g_zall, int64_t n, int S, int n_imp,
                         float* d_weights, nerf_stream_t stream);
 
+/* ERT sample compaction (BASELINE configs[3]): nerf_mlp_forward_x3 over the
+ * flat sample indices list[0 .. *count) (ray * S + step; count read on the
+ * device, max_count bounds it), raw written at those indices. */
+int nerf_mlp_forward_x3_list(const float* w_slices, const float* w_head,
+                             const float* rays_o, const float* rays_d, const float* z,
+                             int64_t z_stride, int S, const int* list, const int* count,
+                             int64_t max_count, float* raw, nerf_stream_t stream);
+
+/* One step of the segmented ERT evaluation: every ray with active[r] extends
+ * its exclusive transmittance T[r] (double) over samples [s0, s1) from raw
+ * with the ERT composite's alpha (VR:1091-1111); once T < thr (1 - 1e-6) it
+ * is retired (its later samples are zero-weighted by _raw2outputs_with_ert,
+ * VR:1115-1123), otherwise it appends the indices of its samples [s1, s2) to
+ * list (slots from *count, atomically). */
+int nerf_ert_segment(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
+                     int64_t n, int S, int s0, int s1, int s2, float thr, double* T,
+                     unsigned char* active, int* list, int* count, nerf_stream_t stream);
+
 /* Training MLP (BASELINE configs[2]): the 8x256 NeRF MLP of a training step
  * (network.py:49-74 forward and its autograd backward) as layer GEMMs over
  * feature-major activations ([F][P]: row f = feature f of every sample),

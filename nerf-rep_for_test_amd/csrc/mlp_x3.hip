@@ -378,11 +378,17 @@ __device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int 
   epi.finish(acc);
 }
 
+// LIST: the samples are the flat indices list[0 .. *count) (ray * S + step,
+// written by the ERT segment kernel; the count is read on the device, so a
+// segmented evaluation needs no host round trip); raw is written at those
+// indices. Otherwise the samples are 0 .. total.
+template <bool LIST>
 __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
-    float4* __restrict__ raw) {
+    float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count) {
+  if constexpr (LIST) total = *count;
   __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
   __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
 
@@ -421,7 +427,8 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const int g4 = lane >> 4;
 #endif
   const bool valid = gs < total;
-  const int64_t gc = valid ? gs : total - 1;
+  const int64_t gl = valid ? gs : total - 1;
+  const int64_t gc = LIST ? (int64_t)list[gl] : gl;   // the flat sample index
   const int64_t ray = gc / S;
   const int step = (int)(gc - ray * S);
   const float zv = z[ray * z_stride + step];
@@ -556,7 +563,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   float rgb[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) rgb[c] = quad_sum(part[c]) + hd[kHeadRgbB + c];
-  if (valid && g4 == 0) raw[gs] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
+  if (valid && g4 == 0) raw[gc] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
   R.rot = (R.rot + kX3Slices) & 3;   // the next tile's slice 0 = this stream's slice 65
   }
 #if MLP_X3_PERSIST
@@ -1184,9 +1191,32 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
 #else
   const int64_t grid = blocks;
 #endif
-  hipLaunchKernelGGL(mlp_x3_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
+  hipLaunchKernelGGL(mlp_x3_kernel<false>, dim3((unsigned)grid), dim3(kX3Threads), 0,
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
-                     z_stride, total, S, (float4*)raw);
+                     z_stride, total, S, (float4*)raw, nullptr, nullptr);
+  return check_launch("mlp_x3_kernel");
+}
+
+extern "C" int nerf_mlp_forward_x3_list(const float* w_slices, const float* w_head,
+                                        const float* rays_o, const float* rays_d, const float* z,
+                                        int64_t z_stride, int S, const int* list,
+                                        const int* count, int64_t max_count, float* raw,
+                                        nerf_stream_t stream) {
+  NERF_REQUIRE(w_slices && w_head && rays_o && rays_d && z && raw && list && count,
+               "nerf_mlp_forward_x3_list: null pointer");
+  NERF_REQUIRE(S >= 1 && z_stride >= 0 && max_count >= 0, "nerf_mlp_forward_x3_list: bad size");
+  NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
+                   ((uintptr_t)raw & 15) == 0,
+               "nerf_mlp_forward_x3_list: weights/raw must be 16-byte aligned");
+  static_assert(MLP_X3_PERSIST, "the list form needs the persistent tile loop");
+  if (max_count == 0) return 0;
+  const int64_t blocks = cdiv(max_count, kX3Tile);
+  NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_forward_x3_list: too many samples");
+  const int n_cu = stream_cu_count(stream);
+  const int64_t grid = blocks < n_cu ? blocks : n_cu;   // persistent: the count is device-side
+  hipLaunchKernelGGL(mlp_x3_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                     as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
+                     z_stride, (int64_t)0, S, (float4*)raw, list, count);
   return check_launch("mlp_x3_kernel");
 }
 

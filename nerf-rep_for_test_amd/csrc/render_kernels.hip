@@ -222,6 +222,56 @@ __global__ __launch_bounds__(64 * ERT_WAVES) void composite_ert_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// ERT sample compaction (C4): the MLP of a pass with ERT runs over depth
+// segments [s0, s1) of the sorted samples; after each, every ray still active
+// carries its exclusive transmittance T over the segment (the composite's own
+// alpha, VR:1091-1111) and is retired once T < thr (1 - 1e-6): every sample
+// from there on is at or after the ray's first low-transmittance sample, whose
+// weight the ERT composite zeroes in any chunk that cuts at all (and this ray
+// makes its chunk cut), so its raw is never read. Active rays append the flat
+// indices of their next segment [s1, s2) to the list the MLP reads next. The
+// margin makes the retirement conservative against the composite's other
+// product order (double accumulation both: ~1e-16 relative). One thread per
+// ray; one atomic per wave for the list slots.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ert_segment_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
+    const float* __restrict__ rays_d, int64_t n, int S, int s0, int s1, int s2, float thr,
+    double* __restrict__ T, unsigned char* __restrict__ active, int* __restrict__ list,
+    int* __restrict__ count) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int want = 0;
+  if (r < n && active[r]) {
+    double t = T[r];
+    if (s1 > s0) {
+      const float* zr = z + r * z_stride;
+      const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
+      for (int s = s0; s < s1; ++s) {
+        const float dist = ((s < S - 1) ? (zr[s + 1] - zr[s]) : 1e10f) * nd;
+        const float a = 1.0f - expf((-fmaxf(raw[r * S + s].w, 0.0f)) * dist);
+        t = t * (double)(1.0f - a);
+      }
+      T[r] = t;
+    }
+    if (t < (double)thr * (1.0 - 1e-6)) active[r] = 0;
+    else want = s2 - s1;
+  }
+  // wave-aggregated slot allocation: exclusive prefix of `want`, one atomic
+  int incl = want;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int q = __shfl_up(incl, o);
+    if (lane >= o) incl += q;
+  }
+  const int total = __shfl(incl, 63);
+  int base = 0;
+  if (lane == 63 && total > 0) base = atomicAdd(count, total);
+  base = __shfl(base, 63);
+  const int off = base + incl - want;
+  for (int k = 0; k < want; ++k) list[off + k] = (int)(r * S + s1 + k);
+}
+
+// ---------------------------------------------------------------------------
 // fine sampling (VR:239-268) + merge with the coarse depths (VR:181-183)
 // one wave per ray, 4 rays per block; per-wave LDS rows
 // ---------------------------------------------------------------------------
@@ -564,6 +614,21 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
 }
 
 extern "C" {
+int nerf_ert_segment(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
+                     int64_t n, int S, int s0, int s1, int s2, float thr, double* T,
+                     unsigned char* active, int* list, int* count, nerf_stream_t stream) {
+  NERF_REQUIRE(raw && z && rays_d && T && active && list && count,
+               "nerf_ert_segment: null pointer");
+  NERF_REQUIRE(n >= 0 && S >= 1 && 0 <= s0 && s0 <= s1 && s1 <= s2 && s2 <= S &&
+                   n * (int64_t)S < (1ll << 31),
+               "nerf_ert_segment: bad segment");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ert_segment_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S, s0, s1, s2,
+                     thr, T, active, list, count);
+  return check_launch("ert_segment_kernel");
+}
+
 
 int nerf_rays(const float* cam, int H, int W, int64_t p0, int64_t n, float* rays_o,
               float* rays_d, nerf_stream_t stream) {

@@ -42,7 +42,8 @@ class NerfPipeline:
     def __init__(self, device, N_samples=64, N_importance=128, near=2.0, far=6.0,
                  lindisp=False, white_bkgd=True, enable_ess=False, enable_ert=False,
                  ert_threshold=0.05, ess_skip_threshold=0.5, grid_update_interval=500,
-                 max_rays_per_pass=1 << 20, mlp_precision="f16x3"):
+                 max_rays_per_pass=1 << 20, mlp_precision="f16x3", ert_compaction=True,
+                 ert_segment=32):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise _lib.NerfHipError("NerfPipeline needs a ROCm GPU device (no CPU fallback)")
@@ -62,6 +63,11 @@ class NerfPipeline:
         if mlp_precision not in MLP_KERNELS:
             raise ValueError(f"mlp_precision must be one of {sorted(MLP_KERNELS)}")
         self.mlp_precision = mlp_precision
+        # ERT passes: the MLP runs depth segment by depth segment and skips the
+        # samples after each ray's termination (x3 kernel only; results identical)
+        self.ert_compaction = bool(ert_compaction)
+        self.ert_segment = int(ert_segment)
+        self.ert_stats = []       # (evaluated-sample counts [segments] device, rays, S) per pass
         self.z_base = coarse_depth_table(self.near, self.far, self.N_samples,
                                          self.lindisp).to(self.device)
         self.u_eval = (torch.linspace(0., 1., steps=self.N_importance).to(self.device)
@@ -115,6 +121,41 @@ class NerfPipeline:
         if t is not None:
             e1.record()
             t.append((e0, e1, n * S, self.mlp_bytes(n, S, z_stride)))
+        return raw
+
+    def mlp_ert(self, packed, rays_o, rays_d, z, z_stride, n, S):
+        """The MLP of an ERT pass over depth segments of ert_segment samples
+        (nerf_ert_segment + nerf_mlp_forward_x3_list, no host round trip): a ray
+        stops being evaluated once its transmittance falls below the threshold,
+        after which _raw2outputs_with_ert zeroes every weight it has
+        (VR:1115-1123); its remaining raw stay 0. The composite then sees exactly
+        the values it reads from a full evaluation."""
+        dev = self.device
+        st = _lib.stream_of(dev)
+        raw = torch.zeros((n * S, 4), device=dev, dtype=torch.float32)
+        T = torch.ones((n,), device=dev, dtype=torch.float64)
+        active = torch.ones((n,), device=dev, dtype=torch.uint8)
+        b = list(range(0, S, self.ert_segment)) + [S]
+        nseg = len(b) - 1
+        counts = torch.zeros((nseg,), device=dev, dtype=torch.int32)
+        lst = torch.empty((n * min(S, self.ert_segment),), device=dev, dtype=torch.int32)
+        t = self.timer
+        for k in range(nseg):
+            s0, s1 = (b[k - 1], b[k]) if k else (0, 0)
+            cnt = counts[k:k + 1]
+            call("nerf_ert_segment", ptr(raw), ptr(z), z_stride, ptr(rays_d), n, S, s0, s1,
+                 b[k + 1], self.ert_threshold, ptr(T), ptr(active), ptr(lst), ptr(cnt), st)
+            if t is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            call("nerf_mlp_forward_x3_list", ptr(packed[0]), ptr(packed[1]), ptr(rays_o),
+                 ptr(rays_d), ptr(z), z_stride, S, ptr(lst), ptr(cnt), n * (b[k + 1] - b[k]),
+                 ptr(raw), st)
+            if t is not None:
+                e1.record()
+                t.append((e0, e1, cnt, None))
+        self.ert_stats.append((counts, n, S))
         return raw
 
     def composite(self, raw, z, z_stride, rays_d, n, S, out, off, need_weights=True):
@@ -172,7 +213,7 @@ class NerfPipeline:
                 zs = S
             else:
                 z, zs = self.z_base, 0                     # one shared row (expand)
-            raw = self.mlp(self.coarse, ro, rd, z, zs, m, S)
+            raw = self._pass_mlp(self.coarse, ro, rd, z, zs, m, S)
             w = self.composite(raw, z, zs, rd, m, S, outputs["coarse"], off + p)
             self._grid_updates(0, counter0, rd, z, zs, raw, w, m, S)
             if NI > 0:
@@ -183,7 +224,7 @@ class NerfPipeline:
                     uu, us = u[p:p + m], NI
                 call("nerf_sample_fine", ptr(z), zs, ptr(w), ptr(uu), us, m, S, NI, ptr(zall), st)
                 del raw, w
-                raw_f = self.mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
+                raw_f = self._pass_mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
                 w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p,
                                      need_weights=self.enable_ert and self.enable_ess)
                 self._grid_updates(1, counter0, rd, zall, S + NI, raw_f, w_f, m, S + NI)
@@ -192,6 +233,20 @@ class NerfPipeline:
                 self.grid_update_counter = counter0 + self._calls_per_chunk() * -(-m // REF_CHUNK)
             p += m
         return outputs
+
+    def _pass_mlp(self, packed, ro, rd, z, zs, m, S):
+        if self.enable_ert and self.ert_compaction and self.mlp_precision == "f16x3":
+            return self.mlp_ert(packed, ro, rd, z, zs, m, S)
+        return self.mlp(packed, ro, rd, z, zs, m, S)
+
+    def evaluated_samples(self, reset=True):
+        """(MLP samples evaluated, samples of a full evaluation) over the ERT
+        passes since the last reset (one host sync)."""
+        ev = sum(int(c.sum()) for c, _, _ in self.ert_stats)
+        full = sum(n * S for _, n, S in self.ert_stats)
+        if reset:
+            self.ert_stats = []
+        return ev, full
 
     def _calls_per_chunk(self):
         return 2 if self.N_importance > 0 else 1

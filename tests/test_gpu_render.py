@@ -442,3 +442,56 @@ def test_sharded_c4_bands_equal_one_pass_frame(dev, counter0):
         for g, c in states:
             assert c == one.grid_update_counter
             assert torch.equal(g, one.grid)
+
+
+@pytest.mark.parametrize("name", ["f3_ert", "f4_ess_ert", "f4b_ess_ert_update", "f3b_ert_noterm"])
+def test_ert_compaction_bitwise_equals_full_evaluation(dev, name):
+    """ERT passes evaluated in depth segments with terminated rays retired
+    (NerfPipeline.mlp_ert) give bitwise the maps, grid and counter of the full
+    evaluation, and skip samples where rays terminate."""
+    z = load(name)
+    outs = {}
+    for comp in (False, True):
+        pipe = _pipe(dev, z, mlp_precision="f16x3", ert_compaction=comp)
+        pipe.set_weights(params_of(z))
+        g = grid_of(z)
+        if g is not None:
+            pipe.set_grid(g)
+        pipe.grid_update_counter = int(z["grid_counter_in"])
+        tr = _t(z["t_rand"], dev) if "t_rand" in z else None
+        res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"], t_rand=tr)
+        outs[comp] = ({k: torch.nan_to_num(v, 7.0) for k, v in res.items()},
+                      None if pipe.grid is None else pipe.grid.clone(), pipe.grid_update_counter,
+                      pipe.evaluated_samples() if comp else None)
+    (a, ga, ca, _), (b, gb, cb, (ev, full)) = outs[False], outs[True]
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert ca == cb
+    assert (ga is None and gb is None) or torch.equal(ga, gb)
+    assert ev <= full
+    # where the reference's chunk decision shows a terminating ray, samples were skipped
+    if bool(z.get("int_chunk_any_0", False)) or bool(z.get("int_chunk_any_1", False)):
+        assert ev < full
+
+
+def test_ert_compaction_frame_with_grid_update(dev):
+    """A 96 x 96 C4 frame (4.5 chunks) whose ESS grid self-updates mid-frame:
+    compacted and full evaluation agree bitwise."""
+    from nerfhip.synthetic import make_occupancy_grid, make_params
+    params = make_params(0, 3.0, 1.0)
+    grid = make_occupancy_grid(4, 128, 0.5, 0.01)
+    cams = load("lego_test_cameras")
+    f = 0.5 * 800 / np.tan(0.5 * float(cams["camera_angle_x"]))
+    K = np.array([[f, 0, 400 - 352], [0, f, 400 - 352], [0, 0, 1]], np.float32)
+    outs = []
+    for comp in (False, True):
+        pipe = _pipe(dev, N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
+                     ert_threshold=0.01, ert_compaction=comp)
+        pipe.set_weights(params)
+        pipe.set_grid(grid)
+        pipe.grid_update_counter = 496
+        res = pipe.render_image(96, 96, cams["poses"][0], K)
+        outs.append(({k: torch.nan_to_num(v, 7.0) for k, v in res.items()}, pipe.grid.clone()))
+    for k in outs[0][0]:
+        assert torch.equal(outs[0][0][k], outs[1][0][k]), k
+    assert torch.equal(outs[0][1], outs[1][1])
