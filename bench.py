@@ -85,6 +85,8 @@ def main():
                          "checkpoints/lego (trained by tools/train_lego.py) when present")
     ap.add_argument("--synthetic", action="store_true",
                     help="synthetic generator weights even when the trained checkpoint exists")
+    ap.add_argument("--no-gt", action="store_true",
+                    help="skip the PSNR/SSIM-vs-ground-truth renders (profiling runs)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 train-step sub-record of the default run")
     ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
@@ -219,7 +221,7 @@ def main():
             result["cpu_baseline"] = torch_cpu_baseline(pipe, H, W, params, 2 * args.cpu_rows,
                                                         result["parity"])
         result["psnr_vs_ref"] = result["parity"]["psnr_fine_rgb"]
-    if rank == 0 and world == 1 and not c4 and os.path.exists(GT_PATH):
+    if rank == 0 and world == 1 and not c4 and not args.no_gt and os.path.exists(GT_PATH):
         result["psnr_vs_gt"] = psnr_vs_gt(pipe, H, W, result.get("parity"))
     del pipe
     if args.precision != "fp32" and not args.no_fp32_run:

@@ -1126,28 +1126,47 @@ struct X3PackDesc {
   int* sw;
 };
 
-__global__ __launch_bounds__(1024) void x3_pack_kernel(const X3PackDesc* __restrict__ descs) {
+// Packing in three launches over (matrix, slab) blocks: the max |W| of every
+// matrix accumulated as float bits into its sw slot (zeroed first), the scale
+// exponent derived from it by every packing block, and the slot rewritten
+// with the exponent by a last one-thread-per-matrix launch.
+constexpr int kPackSlabs = 16;   // blocks per matrix
+
+__global__ void x3_pack_zero_kernel(const X3PackDesc* __restrict__ descs, int n) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < n) *descs[m].sw = 0;
+}
+
+__global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __restrict__ descs) {
   const X3PackDesc d = descs[blockIdx.x];
-  const int tid = threadIdx.x;
-  __shared__ unsigned wg_max;
-  if (tid == 0) wg_max = 0u;
-  __syncthreads();
+  const int total = d.M * d.K;
+  const int per = (total + kPackSlabs - 1) / kPackSlabs;
+  const int i0 = blockIdx.y * per, i1 = min(total, i0 + per);
   float mx = 0.0f;
-  for (int idx = tid; idx < d.M * d.K; idx += 1024) {
+  for (int idx = i0 + (int)threadIdx.x; idx < i1; idx += 256) {
     const int ri = d.rowmap[idx / d.K], ck = d.colmap[idx % d.K];
     if (ri >= 0 && ck >= 0) mx = fmaxf(mx, fabsf(d.src[ri * d.ldr + ck * d.ldc]));
   }
-  atomicMax(&wg_max, __float_as_uint(mx));
-  __syncthreads();
-  const float amax = __uint_as_float(wg_max);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0)   // values >= 0: the float bits order like the floats
+    atomicMax(reinterpret_cast<unsigned*>(d.sw), __float_as_uint(mx));
+}
+
+__device__ __forceinline__ int pack_exponent(float amax) {
   int E = 0;
   if (amax > 0.0f) (void)frexpf(amax, &E);
-  const int sw = amax > 0.0f ? 12 - E : 0;
-  if (tid == 0) *d.sw = sw;
-  const float scale = ldexpf(1.0f, sw);
+  return amax > 0.0f ? 12 - E : 0;   // max |W| 2^sw in [2^11, 2^12)
+}
+
+__global__ __launch_bounds__(256) void x3_pack_kernel(const X3PackDesc* __restrict__ descs) {
+  const X3PackDesc d = descs[blockIdx.x];
+  const float amax = __uint_as_float(*reinterpret_cast<const unsigned*>(d.sw));
+  const float scale = ldexpf(1.0f, pack_exponent(amax));
   const int mt = d.M / 16;
   const int groups = (d.K / 32) * mt * 64;   // (q, t, lane) -> 8 halfs hi + 8 halfs lo
-  for (int gi = tid; gi < groups; gi += 1024) {
+  const int per = (groups + kPackSlabs - 1) / kPackSlabs;
+  const int g0 = blockIdx.y * per, g1 = min(groups, g0 + per);
+  for (int gi = g0 + (int)threadIdx.x; gi < g1; gi += 256) {
     const int lane = gi & 63, qt = gi >> 6;
     const int q = qt / mt, t = qt - q * mt;
     const int row = 16 * t + (lane & 15), k0 = 32 * q + 8 * (lane >> 4);
@@ -1165,6 +1184,11 @@ __global__ __launch_bounds__(1024) void x3_pack_kernel(const X3PackDesc* __restr
     d.out[blk * 64 + lane] = __builtin_bit_cast(uint4, hi);
     d.out[(blk + 1) * 64 + lane] = __builtin_bit_cast(uint4, lo);
   }
+}
+
+__global__ void x3_pack_scale_kernel(const X3PackDesc* __restrict__ descs, int n) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < n) *descs[m].sw = pack_exponent(__uint_as_float(*reinterpret_cast<unsigned*>(descs[m].sw)));
 }
 
 }  // namespace nerfhip
@@ -1293,7 +1317,14 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
 extern "C" int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream) {
   NERF_REQUIRE(descs && n >= 0 && n < 65536, "nerf_x3_pack: bad arguments");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)n), dim3(1024), 0, as_stream(stream),
-                     (const X3PackDesc*)descs);
+  const X3PackDesc* d = (const X3PackDesc*)descs;
+  hipLaunchKernelGGL(x3_pack_zero_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64), 0,
+                     as_stream(stream), d, n);
+  hipLaunchKernelGGL(x3_pack_amax_kernel, dim3((unsigned)n, kPackSlabs), dim3(256), 0,
+                     as_stream(stream), d);
+  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)n, kPackSlabs), dim3(256), 0,
+                     as_stream(stream), d);
+  hipLaunchKernelGGL(x3_pack_scale_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64), 0,
+                     as_stream(stream), d, n);
   return check_launch("x3_pack_kernel");
 }

@@ -5,8 +5,8 @@
 // kernels without data-dependent host syncs (torch's cumprod backward tests its
 // input for zeros on the host, which a HIP graph cannot capture).
 //
-// Compositing: one thread per ray (a training batch is ~1e3 rays x 64-192
-// samples); the transmittance is the reference's exclusive cumprod of
+// Compositing: one wave per ray, lanes over samples; the transmittance is the
+// reference's exclusive cumprod of
 // (1 - a + 1e-10) accumulated in double like torch's CPU kernel, the map sums
 // in torch's CPU summation orders (common.h tsum_last / tsum_dim2).
 // The forward also stores T (the backward reads it instead of dividing w by a).
@@ -30,59 +30,107 @@ namespace nerfhip {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__global__ __launch_bounds__(256) void composite_train_fwd_kernel(
+// One wave per ray (a 1024-ray batch is 1024 waves), lanes over the samples.
+constexpr int CT_WAVES = 4;
+constexpr int CT_MAX_S = 256;
+struct CtLds {
+  float w[CT_MAX_S], z[CT_MAX_S], c[3][CT_MAX_S], gd[CT_MAX_S];
+};
+
+__device__ __forceinline__ double ct_prod_scan(double p, int lane) {   // inclusive
+  for (int o = 1; o < 64; o <<= 1) {
+    const double q = __shfl_up(p, o);
+    if (lane >= o) p *= q;
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(64 * CT_WAVES) void composite_train_fwd_kernel(
     const float4* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rays_d,
     int64_t n, int S, int white, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ depth, float* __restrict__ w,
     float* __restrict__ trans) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
+  __shared__ CtLds sm[CT_WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * CT_WAVES + wave;
+  if (r >= n) return;   // wave-uniform; no block barriers below
+  CtLds& L = sm[wave];
   const float4* rr = raw + r * S;
   const float* zr = z + r * S;
-  float* wr = w + r * S;
-  float* tr = trans + r * S;
   const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
   double carry = 1.0;
-  for (int s = 0; s < S; ++s) {
-    const float zs = zr[s];
-    const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;     // VR:290-292
-    const float a = 1.0f - expf((-fmaxf(rr[s].w, 0.0f)) * dist);          // VR:288
-    const float T = (float)carry;
-    tr[s] = T;
-    wr[s] = a * T;                                                         // VR:329
-    carry = carry * (double)((1.0f - a) + 1e-10f);
+  for (int b = 0; b < S; b += 64) {
+    const int s = b + lane;
+    const bool act = s < S;
+    float a = 0.0f, zs = 0.0f;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (act) {
+      v = rr[s];
+      zs = zr[s];
+      const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;   // VR:290-292
+      a = 1.0f - expf((-fmaxf(v.w, 0.0f)) * dist);                       // VR:288
+    }
+    // exclusive cumprod of (1 - a + 1e-10), accumulated in double (VR:329)
+    const double inc = ct_prod_scan(act ? (double)((1.0f - a) + 1e-10f) : 1.0, lane);
+    double ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = 1.0;
+    const float T = (float)(carry * ex);
+    carry = carry * __shfl(inc, 63);
+    if (act) {
+      const float ws = a * T;
+      w[r * S + s] = ws;
+      trans[r * S + s] = T;
+      L.w[s] = ws;
+      L.z[s] = zs;
+      L.c[0][s] = ws * sigm(v.x);
+      L.c[1][s] = ws * sigm(v.y);
+      L.c[2][s] = ws * sigm(v.z);
+    }
   }
-  float m[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-    m[c] = tsum_dim2(S, [&](int s) {
-      const float4 v = rr[s];
-      return wr[s] * sigm(c == 0 ? v.x : (c == 1 ? v.y : v.z));
-    });
-  const float dp = tsum_last(S, [&](int s) { return wr[s] * zr[s]; });
-  const float ac = tsum_last(S, [&](int s) { return wr[s]; });
-  disp[r] = 1.0f / torch_max(1e-10f, dp / ac);
-  acc[r] = ac;
-  depth[r] = dp;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) rgb[r * 3 + c] = white ? m[c] + (1.0f - ac) : m[c];
+  __builtin_amdgcn_wave_barrier();
+  // the map sums in torch's CPU orders, one lane per sum (VR:331-334)
+  float m = 0.0f;
+  if (lane < 3) {
+    const float* cr = L.c[lane];
+    m = tsum_dim2(S, [&](int i) { return cr[i]; });
+  } else if (lane == 3) {
+    m = tsum_last(S, [&](int i) { return L.w[i] * L.z[i]; });
+  } else if (lane == 4) {
+    m = tsum_last(S, [&](int i) { return L.w[i]; });
+  }
+  const float m0 = __shfl(m, 0), m1 = __shfl(m, 1), m2 = __shfl(m, 2);
+  const float dp = __shfl(m, 3), ac = __shfl(m, 4);
+  if (lane == 0) {
+    disp[r] = 1.0f / torch_max(1e-10f, dp / ac);
+    acc[r] = ac;
+    depth[r] = dp;
+    rgb[r * 3 + 0] = white ? m0 + (1.0f - ac) : m0;
+    rgb[r * 3 + 1] = white ? m1 + (1.0f - ac) : m1;
+    rgb[r * 3 + 2] = white ? m2 + (1.0f - ac) : m2;
+  }
 }
 
 // Gradients: g_rgb [n,3], g_disp / g_acc / g_depth [n], g_w [n,S] (any may be
 // null = zero). Outputs d_raw [n,S,4] and d_z [n,S] (null: not needed).
-__global__ __launch_bounds__(256) void composite_train_bwd_kernel(
+// B_{s-1} = h_s(B_s) with h_s(x) = G_s a_s + x_s x and B_{S-1} = 0: per 64-sample
+// block (from the last), a reverse inclusive scan composes the affine maps
+// (double), lane i applies the composition from i+1 up to the carried B.
+__global__ __launch_bounds__(64 * CT_WAVES) void composite_train_bwd_kernel(
     const float4* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rays_d,
     const float* __restrict__ w, const float* __restrict__ trans, const float* __restrict__ acc,
-    const float* __restrict__ depth,
-    int64_t n, int S, int white, const float* __restrict__ g_rgb,
-    const float* __restrict__ g_disp, const float* __restrict__ g_acc,
-    const float* __restrict__ g_depth, const float* __restrict__ g_w, float4* __restrict__ d_raw,
-    float* __restrict__ d_z) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const float* __restrict__ depth, int64_t n, int S, int white,
+    const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
+    const float* __restrict__ g_acc, const float* __restrict__ g_depth,
+    const float* __restrict__ g_w, float4* __restrict__ d_raw, float* __restrict__ d_z) {
+  __shared__ CtLds sm[CT_WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * CT_WAVES + wave;
   if (r >= n) return;
+  CtLds& L = sm[wave];
   const float4* rr = raw + r * S;
   const float* zr = z + r * S;
-  const float* wr = w + r * S;
   const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
   float gr[3] = {0.f, 0.f, 0.f};
   if (g_rgb) for (int c = 0; c < 3; ++c) gr[c] = g_rgb[r * 3 + c];
@@ -97,40 +145,61 @@ __global__ __launch_bounds__(256) void composite_train_bwd_kernel(
       ga -= gq * dp / (ac * ac);
     }
   }
-  float* dzr = d_z ? d_z + r * S : nullptr;
-  if (dzr) for (int s = 0; s < S; ++s) dzr[s] = 0.0f;
-  // reverse sweep: B_s = sum_{j>s} G_j a_j prod_{s<k<j} x_k
-  float B = 0.0f;
-  for (int s = S - 1; s >= 0; --s) {
-    const float4 v = rr[s];
-    const float zs = zr[s];
-    const float dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;
-    const float sig = fmaxf(v.w, 0.0f);
-    const float e = expf(-sig * dist);
-    const float a = 1.0f - e;
-    const float ws = wr[s];
-    const float c0 = sigm(v.x), c1 = sigm(v.y), c2 = sigm(v.z);
-    const float G = (g_w ? g_w[r * S + s] : 0.0f) + gr[0] * c0 + gr[1] * c1 + gr[2] * c2 + ga +
-                    gd * zs;
-    const float T = trans[r * S + s];
-    const float ga_s = T * (G - B);                     // dL/da_s
-    // a = 1 - exp(-relu(r3) d): da/dr3 = d e (r3 > 0), da/dd = relu(r3) e
-    const float g_sig = v.w > 0.0f ? ga_s * dist * e : 0.0f;
-    float4 dr;
-    dr.x = ws * gr[0] * c0 * (1.0f - c0);
-    dr.y = ws * gr[1] * c1 * (1.0f - c1);
-    dr.z = ws * gr[2] * c2 * (1.0f - c2);
-    dr.w = g_sig;
-    d_raw[r * S + s] = dr;
-    if (dzr) {
-      dzr[s] += ws * gd;                                  // depth = sum w z
-      if (s < S - 1) {
-        const float g_dist = ga_s * sig * e * nd;         // dist = (z[s+1] - z[s]) |d|
-        dzr[s + 1] += g_dist;
-        dzr[s] -= g_dist;
+  double carry = 0.0;   // B at the top index of the block being processed
+  for (int b = ((S - 1) / 64) * 64; b >= 0; b -= 64) {
+    const int s = b + lane;
+    const bool act = s < S;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    float zs = 0.f, dist = 0.f, sig = 0.f, e = 1.f, a = 0.f, ws = 0.f, T = 0.f, G = 0.f;
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+    if (act) {
+      v = rr[s];
+      zs = zr[s];
+      dist = ((s < S - 1) ? (zr[s + 1] - zs) : 1e10f) * nd;
+      sig = fmaxf(v.w, 0.0f);
+      e = expf(-sig * dist);
+      a = 1.0f - e;
+      ws = w[r * S + s];
+      T = trans[r * S + s];
+      c0 = sigm(v.x);
+      c1 = sigm(v.y);
+      c2 = sigm(v.z);
+      G = (g_w ? g_w[r * S + s] : 0.0f) + gr[0] * c0 + gr[1] * c1 + gr[2] * c2 + ga + gd * zs;
+    }
+    // h_s = (m, c) = (x_s, G_s a_s); identity past the last sample
+    double hm = act ? (double)((1.0f - a) + 1e-10f) : 1.0;
+    double hc = act ? (double)G * (double)a : 0.0;
+    // reverse inclusive scan: H_s = h_s o h_{s+1} o ... (lane' = 63 - lane)
+    double M = __shfl(hm, 63 - lane), C = __shfl(hc, 63 - lane);
+    for (int o = 1; o < 64; o <<= 1) {
+      const double Mo = __shfl_up(M, o), Co = __shfl_up(C, o);
+      if (lane >= o) {   // (this) o (earlier lanes' = higher indices)
+        C = C + M * Co;
+        M = M * Mo;
       }
     }
-    B = G * a + ((1.0f - a) + 1e-10f) * B;               // B_{s-1}
+    // back to index order: H at lane i; B_i = H_{i+1}(carry), B_top = carry
+    const double Mi = __shfl(M, 63 - lane), Ci = __shfl(C, 63 - lane);
+    double Mn = __shfl_down(Mi, 1), Cn = __shfl_down(Ci, 1);
+    if (lane == 63) { Mn = 1.0; Cn = 0.0; }
+    const float B = (float)(Cn + Mn * carry);
+    carry = __shfl(Ci, 0) + __shfl(Mi, 0) * carry;   // B_{b-1}
+    if (act) {
+      const float ga_s = T * (G - B);                    // dL/da_s
+      float4 dr;
+      dr.x = ws * gr[0] * c0 * (1.0f - c0);
+      dr.y = ws * gr[1] * c1 * (1.0f - c1);
+      dr.z = ws * gr[2] * c2 * (1.0f - c2);
+      dr.w = v.w > 0.0f ? ga_s * dist * e : 0.0f;       // da/dr3 = d e where r3 > 0
+      d_raw[r * S + s] = dr;
+      L.gd[s] = (s < S - 1) ? ga_s * sig * e * nd : 0.0f;   // dL/d(z[s+1] - z[s])
+      L.w[s] = ws;
+    }
+  }
+  if (d_z) {
+    __builtin_amdgcn_wave_barrier();
+    for (int s = lane; s < S; s += 64)
+      d_z[r * S + s] = L.w[s] * gd - L.gd[s] + (s > 0 ? L.gd[s - 1] : 0.0f);
   }
 }
 
@@ -299,9 +368,10 @@ int nerf_composite_train_fwd(const float* raw, const float* z, const float* rays
                              float* weights, float* trans, nerf_stream_t stream) {
   NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth && weights && trans,
                "nerf_composite_train_fwd: null pointer");
-  NERF_REQUIRE(n >= 0 && S >= 1 && S < 1024, "nerf_composite_train_fwd: bad size");
+  NERF_REQUIRE(n >= 0 && S >= 1 && S <= CT_MAX_S, "nerf_composite_train_fwd: bad size");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(composite_train_fwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(composite_train_fwd_kernel, dim3((unsigned)cdiv(n, CT_WAVES)),
+                     dim3(64 * CT_WAVES), 0,
                      as_stream(stream), (const float4*)raw, z, rays_d, n, S, white, rgb, disp,
                      acc, depth, weights, trans);
   return check_launch("composite_train_fwd_kernel");
@@ -315,9 +385,10 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
                              float* d_raw, float* d_z, nerf_stream_t stream) {
   NERF_REQUIRE(raw && z && rays_d && weights && trans && acc && depth && d_raw,
                "nerf_composite_train_bwd: null pointer");
-  NERF_REQUIRE(n >= 0 && S >= 1 && S < 1024, "nerf_composite_train_bwd: bad size");
+  NERF_REQUIRE(n >= 0 && S >= 1 && S <= CT_MAX_S, "nerf_composite_train_bwd: bad size");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(composite_train_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(composite_train_bwd_kernel, dim3((unsigned)cdiv(n, CT_WAVES)),
+                     dim3(64 * CT_WAVES), 0,
                      as_stream(stream), (const float4*)raw, z, rays_d, weights, trans, acc, depth,
                      n, S,
                      white, g_rgb, g_disp, g_acc, g_depth, g_weights, (float4*)d_raw, d_z);
