@@ -176,7 +176,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         timer, pipe.timer = pipe.timer, None
-        return pipe, elapsed, roofline(precision, timer, elapsed, world, H, W)
+        return pipe, elapsed, roofline(precision, timer, elapsed, world, H, W,
+                                       pmc_workload=world == 1 and not c4)
 
     pipe, elapsed, roof = measure(args.precision)
     rays = H * W * args.steps
@@ -339,9 +340,11 @@ DTYPES = {"fp32": "fp32",
           "f16x3": "fp32 operands as 3-term fp16 splits on fp16 mfma, fp32 accumulate"}
 
 
-def roofline(precision, timer, elapsed, world, H, W):
+def roofline(precision, timer, elapsed, world, H, W, pmc_workload=True):
     """Dominant kernel (the fused MLP: coarse + fine launches), timed by HIP events
-    recorded on the stream it is launched on."""
+    recorded on the stream it is launched on. pmc_workload: the launches are the
+    whole-frame C2 launches the committed PMC summary measured (else traffic is
+    null: band or ERT-compacted launches were not counted)."""
     from nerfhip.render import NerfPipeline
     mlp_ms = sum(a.elapsed_time(b) for a, b, _, _ in timer)
     # ERT-compacted launches record their device-side sample count (resolved here,
@@ -365,7 +368,7 @@ def roofline(precision, timer, elapsed, world, H, W):
             "frac": achieved / peak,
             "algorithmic_tflops": algo_tflops,
             "frac_of_fp32_peak": algo_tflops / FP32_MFMA_PEAK_TFLOPS,
-            "traffic": pmc_traffic(H, W, kernel),
+            "traffic": pmc_traffic(H, W, kernel) if pmc_workload else None,
             "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
             "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
             "launches": n_launch,

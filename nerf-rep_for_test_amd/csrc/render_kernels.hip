@@ -273,25 +273,60 @@ __global__ __launch_bounds__(256) void ert_segment_kernel(
 
 // ---------------------------------------------------------------------------
 // fine sampling (VR:239-268) + merge with the coarse depths (VR:181-183)
-// one wave per ray, 4 rays per block; per-wave LDS rows
+// 16 lanes per ray (4 rays per wave, 16 per block), so that four times the rays
+// of a one-wave-per-ray layout are in flight: the kernel is a chain of short
+// dependent LDS steps per ray, latency- not bandwidth-bound. Each lane carries
+// its ray's searches together through a fixed-step (branch-free) binary
+// search, so a search costs ~log2(S) LDS latencies for all of them.
+// Per-ray LDS row (dynamic): zc[S] | cdf[S] | zf[max(p2, S - 2)] (+ padding),
+// the weights (+1e-5) staged in the zf slot until the cdf is built.
 // ---------------------------------------------------------------------------
+constexpr int FINE_LANES = 16;                    // lanes per ray
+constexpr int FINE_RPW = 64 / FINE_LANES;         // rays per wave
 constexpr int FINE_WAVES = 4;
-constexpr int FINE_MAX_S = 130;      // coarse samples per ray
-constexpr int FINE_MAX_IMP = 256;    // fine samples per ray
-constexpr int FINE_ROW = FINE_MAX_S + 2;
+constexpr int FINE_RPB = FINE_RPW * FINE_WAVES;   // rays per block
+constexpr int FINE_MAX_S = 130;                   // coarse samples per ray
+constexpr int FINE_MAX_IMP = 256;                 // fine samples per ray
 
-struct FineLds {
-  float zc[FINE_ROW];        // coarse depths (sorted)
-  float wv[FINE_ROW];        // weights[1:-1] + 1e-5
-  float cdf[FINE_ROW];       // [0, cumsum(pdf)]
-  float bins[FINE_ROW];      // mids of z
-  float zf[FINE_MAX_IMP];    // fine samples, sorted in place
-};
+__host__ __device__ __forceinline__ int fine_p2(int n_imp) {
+  int p2 = FINE_LANES;
+  while (p2 < n_imp) p2 <<= 1;
+  return p2;
+}
 
-// torch.sum(x, -1) in ATen's order (common.h tsum_last), computed by the whole
-// wave: lane l < 8 folds vector lane l's four accumulators, the scalar tail and
-// the final in-order combination are evaluated redundantly by every lane.
-__device__ __forceinline__ float wave_tsum_last(const float* v, int n, int lane) {
+// Q searches per lane over the ascending a[0..n) (n >= 1): pos[q] =
+// #{a[i] <= x[q]} (UPPER, searchsorted right=True) or #{a[i] < x[q]}.
+// Branch-free halving (the window [base, base + len) always holds the answer's
+// boundary and never leaves a[0..n)): the step count depends on n only, and
+// every step issues all the lane's LDS reads before any is consumed.
+template <bool UPPER, int Q>
+__device__ __forceinline__ void fine_search(const float* a, int n, const float (&x)[Q],
+                                            int (&pos)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q) pos[q] = 0;
+  int len = n;
+  while (len > 1) {
+    const int half = len >> 1;
+    float v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = a[pos[q] + half - 1];
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (UPPER ? v[q] <= x[q] : v[q] < x[q]) pos[q] += half;
+    len -= half;
+  }
+  float v[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) v[q] = a[pos[q] + len - 1];
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (UPPER ? v[q] <= x[q] : v[q] < x[q]) pos[q] += len;
+}
+
+// torch.sum(x, -1) in ATen's order (common.h tsum_last) by a 16-lane group:
+// lane t < 8 folds vector lane t's four accumulators; the scalar tail and the
+// in-order combination are evaluated redundantly by every lane of the group.
+__device__ __forceinline__ float group_tsum_last(const float* v, int n, int lane) {
   if (n < 8) return tsum_last(n, [&](int i) { return v[i]; });
   const int nv = n >> 3, nilp = nv >> 2, l = lane & 7;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -306,119 +341,136 @@ __device__ __forceinline__ float wave_tsum_last(const float* v, int n, int lane)
   const float part = ((a0 + a1) + a2) + a3;
   float fin = 0.f;
   for (int k = nv * 8; k < n; ++k) fin = fin + v[k];
+  const int base = lane & ~(FINE_LANES - 1);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) fin = fin + __shfl(part, q);
+  for (int q = 0; q < 8; ++q) fin = fin + __shfl(part, base + q);
   return fin;
 }
 
-__device__ __forceinline__ double wave_sum_scan(double p, int lane) {   // inclusive
-  for (int o = 1; o < 64; o <<= 1) {
-    const double q = __shfl_up(p, o);
-    if (lane >= o) p += q;
-  }
-  return p;
-}
-
-// number of a[0..n) < x  (a ascending)
-__device__ __forceinline__ int lower_bound(const float* a, int n, float x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-// number of a[0..n) <= x
-__device__ __forceinline__ int upper_bound(const float* a, int n, float x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
+// QN / CN: fine / coarse samples per lane the instance is unrolled for
+// (>= ceil(n_imp / 16), ceil(S / 16)); the launcher picks the smallest.
+template <int QN, int CN>
 __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
     const float* __restrict__ z, int64_t z_stride, const float* __restrict__ weights,
-    const float* __restrict__ u, int64_t u_stride, int64_t n, int S, int n_imp,
+    const float* __restrict__ u, int64_t u_stride, int64_t n, int S, int n_imp, int row_len,
     float* __restrict__ z_all) {
-  __shared__ FineLds sm[FINE_WAVES];
+  extern __shared__ float fine_sm[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t ray = (int64_t)blockIdx.x * FINE_WAVES + wave;
-  if (ray >= n) return;   // wave-uniform; no block barriers below
-  FineLds& L = sm[wave];
-  const float* zr = z + ray * z_stride;
-  const float* wr = weights + ray * S;
-  const int nb = S - 1;       // bins = mids of z; the cdf has nb entries
-  const int nw = S - 2;       // weights[..., 1:-1]
-  for (int s = lane; s < S; s += 64) L.zc[s] = zr[s];
-  for (int s = lane; s < nw; s += 64) L.wv[s] = wr[s + 1] + 1e-5f;
+  const int t = lane & (FINE_LANES - 1);
+  const int row = threadIdx.x / FINE_LANES;   // ray within the block
+  const int64_t wave_ray0 = ((int64_t)blockIdx.x * FINE_WAVES + (threadIdx.x >> 6)) * FINE_RPW;
+  if (wave_ray0 >= n) return;   // wave-uniform; no block barriers below
+  const int64_t ray = wave_ray0 + (lane / FINE_LANES);
+  const bool live = ray < n;    // rays past n (last wave only) run on dummy data
+  const int nb = S - 1;         // bins = mids of z; the cdf has nb entries
+  const int nw = S - 2;         // weights[..., 1:-1]
+  const int p2 = fine_p2(n_imp);
+  float* zc = fine_sm + (size_t)row * row_len;
+  float* cdf = zc + S;
+  float* zf = cdf + S;          // also the staged weights (wv) until the cdf is built
+  const float* zr = z + (live ? ray : 0) * z_stride;
+  const float* wr = weights + (live ? ray : 0) * S;
+  for (int s = t; s < S; s += FINE_LANES) zc[s] = live ? zr[s] : (float)s;
+  for (int s = t; s < nw; s += FINE_LANES) zf[s] = (live ? wr[s + 1] : 0.0f) + 1e-5f;
   __builtin_amdgcn_wave_barrier();
-  for (int s = lane; s < nb; s += 64) L.bins[s] = 0.5f * (L.zc[s + 1] + L.zc[s]);
   // pdf = w / torch.sum(w, -1); cdf = [0, cumsum(pdf)] accumulated in double
-  const float tot = wave_tsum_last(L.wv, nw, lane);
-  double carry = 0.0;
-  if (lane == 0) L.cdf[0] = 0.0f;
-  for (int b = 0; b < nw; b += 64) {
-    const int s = b + lane;
-    const double pdf = s < nw ? (double)(L.wv[s] / tot) : 0.0;
-    const double inc = carry + wave_sum_scan(pdf, lane);
-    if (s < nw) L.cdf[s + 1] = (float)inc;
-    carry = __shfl(inc, 63);
+  // (exact in any order: every pdf is a float in (2^-24, 1], the sums < 2)
+  const float tot = group_tsum_last(zf, nw, lane);
+  const int pc = (nw + FINE_LANES - 1) / FINE_LANES;   // weights per lane, contiguous
+  const int s0 = t * pc;
+  double pdf[CN];
+  double own = 0.0;
+#pragma unroll
+  for (int k = 0; k < CN; ++k) {
+    const int s = s0 + k;
+    pdf[k] = (k < pc && s < nw) ? (double)(zf[s] / tot) : 0.0;
+    own += pdf[k];
+  }
+  double incl = own;
+#pragma unroll
+  for (int o = 1; o < FINE_LANES; o <<= 1) {
+    const double q = __shfl_up(incl, o, FINE_LANES);
+    if (t >= o) incl += q;
+  }
+  double run = incl - own;   // exact (see above)
+  __builtin_amdgcn_wave_barrier();
+  if (t == 0) cdf[0] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < CN; ++k) {
+    const int s = s0 + k;
+    run += pdf[k];
+    if (k < pc && s < nw) cdf[s + 1] = (float)run;
   }
   __builtin_amdgcn_wave_barrier();
-  // inverse CDF (searchsorted right=True, clamp, lerp; VR:254-266)
-  const float* ur = u + ray * u_stride;
-  int p2 = 64;
-  while (p2 < n_imp) p2 <<= 1;
-  for (int j = lane; j < p2; j += 64) {
-    float v = __builtin_inff();
-    if (j < n_imp) {
-      const float uj = ur[j];
-      const int inds = upper_bound(L.cdf, nb, uj);
-      const int below = inds - 1 > 0 ? inds - 1 : 0;
-      const int above = inds < nb - 1 ? inds : nb - 1;
-      const float cg0 = L.cdf[below], cg1 = L.cdf[above];
-      const float bg0 = L.bins[below], bg1 = L.bins[above];
-      float denom = cg1 - cg0;
-      denom = denom < 1e-5f ? 1.0f : denom;
-      const float t = (uj - cg0) / denom;
-      v = bg0 + t * (bg1 - bg0);
-    }
-    L.zf[j] = v;
+  // inverse CDF (searchsorted right=True, clamp, lerp; VR:254-266); fine sample
+  // j = t + 16 q of this lane
+  const float* ur = u + (live ? ray : 0) * u_stride;
+  const int nq = t < n_imp ? (n_imp - 1 - t) / FINE_LANES + 1 : 0;
+  float x[QN];
+  int pos[QN];
+#pragma unroll
+  for (int q = 0; q < QN; ++q) x[q] = q < nq ? ur[t + FINE_LANES * q] : 0.0f;
+  fine_search<true>(cdf, nb, x, pos);
+#pragma unroll
+  for (int q = 0; q < QN; ++q) {   // (queries q >= nq run on u = 0 and are never stored)
+    const int inds = pos[q];
+    const int below = inds - 1 > 0 ? inds - 1 : 0;
+    const int above = inds < nb - 1 ? inds : nb - 1;
+    const float cg0 = cdf[below], cg1 = cdf[above];
+    const float bg0 = 0.5f * (zc[below + 1] + zc[below]);
+    const float bg1 = 0.5f * (zc[above + 1] + zc[above]);
+    float denom = cg1 - cg0;
+    denom = denom < 1e-5f ? 1.0f : denom;
+    const float tt = (x[q] - cg0) / denom;
+    x[q] = bg0 + tt * (bg1 - bg0);
   }
+  __builtin_amdgcn_wave_barrier();   // every read of the staged weights is done
+#pragma unroll
+  for (int q = 0; q < QN; ++q)
+    if (q < nq) zf[t + FINE_LANES * q] = x[q];
+  for (int j = n_imp + t; j < p2; j += FINE_LANES) zf[j] = __builtin_inff();
   __builtin_amdgcn_wave_barrier();
-  // ascending bitonic sort of the (inf-padded) fine samples, skipped when the
-  // inverse CDF of sorted u (eval: linspace) already produced them in order
+  // ascending bitonic sort of the (inf-padded) fine samples, per ray, skipped
+  // when the inverse CDF of sorted u (eval: linspace) already produced them in
+  // order
   bool unsorted = false;
-  for (int j = lane; j + 1 < n_imp; j += 64) unsorted |= L.zf[j] > L.zf[j + 1];
-  if (__ballot(unsorted)) {
+  for (int j = t; j + 1 < n_imp; j += FINE_LANES) unsorted |= zf[j] > zf[j + 1];
+  const unsigned long long bal = __ballot(unsorted);
+  if ((bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull) {
     for (int k = 2; k <= p2; k <<= 1) {
       for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = lane; i < p2; i += 64) {
+        for (int i = t; i < p2; i += FINE_LANES) {
           const int prt = i ^ jj;
           if (prt > i) {
-            const float x = L.zf[i], y = L.zf[prt];
+            const float a = zf[i], b = zf[prt];
             const bool up = (i & k) == 0;
-            if ((x > y) == up) { L.zf[i] = y; L.zf[prt] = x; }
+            if ((a > b) == up) { zf[i] = b; zf[prt] = a; }
           }
         }
         __builtin_amdgcn_wave_barrier();
       }
     }
+#pragma unroll
+    for (int q = 0; q < QN; ++q)
+      if (q < nq) x[q] = zf[t + FINE_LANES * q];
   }
   // torch.sort(cat(z, z_fine)) values: merge by rank (ties: coarse first; equal
   // values are interchangeable)
+  const int ncl = t < S ? (S - 1 - t) / FINE_LANES + 1 : 0;
+  float xc[CN];
+  int pcz[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) xc[c] = c < ncl ? zc[t + FINE_LANES * c] : 0.0f;
+  fine_search<false>(zf, n_imp, xc, pcz);
+  fine_search<true>(zc, S, x, pos);
+  if (!live) return;
   float* out = z_all + ray * (int64_t)(S + n_imp);
-  for (int i = lane; i < S; i += 64) {
-    const float x = L.zc[i];
-    out[i + lower_bound(L.zf, n_imp, x)] = x;
-  }
-  for (int j = lane; j < n_imp; j += 64) {
-    const float x = L.zf[j];
-    out[j + upper_bound(L.zc, S, x)] = x;
-  }
+#pragma unroll
+  for (int c = 0; c < CN; ++c)
+    if (c < ncl) out[t + FINE_LANES * c + pcz[c]] = xc[c];
+#pragma unroll
+  for (int q = 0; q < QN; ++q)
+    if (q < nq) out[t + FINE_LANES * q + pos[q]] = x[q];
 }
 
 // ---------------------------------------------------------------------------
@@ -686,8 +738,27 @@ int nerf_sample_fine(const float* z, int64_t z_stride, const float* weights, con
   NERF_REQUIRE(n >= 0 && S >= 3 && S <= FINE_MAX_S && n_imp >= 1 && n_imp <= FINE_MAX_IMP,
                "nerf_sample_fine: need 3 <= S <= 130 coarse and 1 <= n_imp <= 256 fine samples");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(sample_fine_kernel, dim3((unsigned)cdiv(n, FINE_WAVES)), dim3(64 * FINE_WAVES), 0,
-                     as_stream(stream), z, z_stride, weights, u, u_stride, n, S, n_imp, z_all);
+  // row: zc[S] | cdf[S] | zf, padded so rays sit 16 floats apart mod 32 banks:
+  // the two rays of a ds_read_b32 lane group hit disjoint banks on aligned runs
+  const int p2 = fine_p2(n_imp);
+  int row = 2 * S + (p2 > S - 2 ? p2 : S - 2);
+  row += (48 - row % 32) % 32;
+  const int q = (int)cdiv(n_imp, FINE_LANES), c = (int)cdiv(S, FINE_LANES);
+  const dim3 grid((unsigned)cdiv(n, FINE_RPB)), block(64 * FINE_WAVES);
+  const size_t lds = FINE_RPB * (size_t)row * sizeof(float);
+#define NERF_FINE_LAUNCH(QN, CN)                                                          \
+  hipLaunchKernelGGL((sample_fine_kernel<QN, CN>), grid, block, lds, as_stream(stream), z, \
+                     z_stride, weights, u, u_stride, n, S, n_imp, row, z_all)
+#define NERF_FINE_C(QN)                          \
+  if (c <= 2) NERF_FINE_LAUNCH(QN, 2);           \
+  else if (c <= 4) NERF_FINE_LAUNCH(QN, 4);      \
+  else NERF_FINE_LAUNCH(QN, 9);
+  if (q <= 2) { NERF_FINE_C(2) }
+  else if (q <= 4) { NERF_FINE_C(4) }
+  else if (q <= 8) { NERF_FINE_C(8) }
+  else { NERF_FINE_C(16) }
+#undef NERF_FINE_C
+#undef NERF_FINE_LAUNCH
   return check_launch("sample_fine_kernel");
 }
 

@@ -1,6 +1,6 @@
 """HBM roofline of the byte-moving kernels (GPU): algorithmic bytes / HIP-event time.
 
-    python tools/hbm_bench.py [out.json]
+    python tools/hbm_bench.py [out.json] [only]   # only: "composite" or "sample_fine"
 
 Each case: inputs resident in HBM, 3 warm-up launches, then the median of 10
 launches timed with events on torch's current stream (the stream the kernels
@@ -52,7 +52,8 @@ def main():
 
     n = 640000
     rd = torch.nn.functional.normalize(torch.randn(n, 3, device=dev, generator=g), dim=1)
-    for S, shared, wts in ((64, True, True), (192, False, False)):
+    only = sys.argv[2] if len(sys.argv) > 2 else None
+    for S, shared, wts in ((64, True, True), (192, False, False)) if only in (None, "composite") else ():
         raw = torch.randn(n * S, 4, device=dev, generator=g)
         z = (torch.sort(torch.rand(n, S, device=dev, generator=g) * 4 + 2, 1)[0]
              if not shared else torch.linspace(2, 6, S, device=dev))
@@ -77,6 +78,11 @@ def main():
                            ptr(zall), st))
     report("sample_fine S=64 NI=128", n * S * 4 + n * (S + NI) * 4, t,
            "coarse weights 4 B/sample in + merged depths 4 B/sample out (shared z row, u)")
+    if only is not None:
+        for _ in range(20):   # a longer run for PMC passes
+            call("nerf_sample_fine", ptr(zc), 0, ptr(wc), ptr(u), 0, n, S, NI, ptr(zall), st)
+        torch.cuda.synchronize()
+        return
 
     ro = torch.zeros(n, 3, device=dev)
     cam = torch.eye(4, device=dev).reshape(-1)
