@@ -177,7 +177,9 @@ class Renderer:
         """Training-mode render (VR:109-268 with self.net.training): rays and
         coarse depths from the HIP kernels, both MLPs forward + backward on the
         x3 MFMA training kernels (cfg ``train_mlp``: "x3", default, or "torch"),
-        compositing / importance sampling / ERT in torch autograd; the reference's
+        compositing and importance sampling on the HIP training ops
+        (nerfhip/train_ops.py; with ERT the chunk-rule composite of
+        nerfhip.train.composite_ert); the reference's
         RNG order per 2048-ray chunk (perturb draw, then fine u) and its ESS/ERT
         chunk semantics (nerfhip.train.render_rays_train)."""
         from nerfhip.train import query, render_rays_train
