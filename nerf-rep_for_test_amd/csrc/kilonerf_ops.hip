@@ -321,7 +321,8 @@ __global__ __launch_bounds__(RS_BLOCK) void rs_scatter_kernel(
 // ---------------------------------------------------------------------------
 // per-network segments: offsets passed by value, 128 networks per launch
 // ---------------------------------------------------------------------------
-constexpr int SEG_BATCH = 128;
+constexpr int SEG_BATCH = 448;   // networks per launch: the offsets travel as a
+                                  // kernel argument (3.6 KB, under the 4 KB kernarg budget)
 struct SegBatch {
   int count;
   int64_t off[SEG_BATCH + 1];   // row offsets (relative to the whole batch input)
@@ -360,8 +361,8 @@ __global__ void kn_g2l_kernel(float* __restrict__ pts, const float* __restrict__
   }
 }
 
-// grouped GEMM: one thread per output element, fma chain over k (MAGMA's
-// order is unknown: parity unpinned)
+// grouped GEMM fallback for shapes beyond the MFMA kernels' LDS budget: one
+// thread per output element, fma chain over k
 __global__ void kn_grouped_gemm_kernel(int mode, const float* __restrict__ bias,
                                        const float* __restrict__ X, const float* __restrict__ W,
                                        int out_f, int in_f, float* __restrict__ out, SegBatch sb,
@@ -385,16 +386,6 @@ __global__ void kn_grouped_gemm_kernel(int mode, const float* __restrict__ bias,
   out[row * out_f + col] = acc;
 }
 
-__global__ void kn_row_sum_kernel(const float* __restrict__ M, int64_t cols,
-                                  float* __restrict__ out, SegBatch sb, int net0) {
-  const int k = blockIdx.y;
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.0f;
-  for (int64_t r = sb.off[k]; r < sb.off[k + 1]; ++r) s = s + M[r * cols + c];
-  out[(int64_t)(net0 + k) * cols + c] = s;
-}
-
 __global__ void kn_at_b_kernel(const float* __restrict__ A, int64_t ac, const float* __restrict__ B,
                                int64_t bc, float* __restrict__ out, SegBatch sb, int net0) {
   const int k = blockIdx.y;
@@ -404,6 +395,166 @@ __global__ void kn_at_b_kernel(const float* __restrict__ A, int64_t ac, const fl
   float s = 0.0f;
   for (int64_t r = sb.off[k]; r < sb.off[k + 1]; ++r) s = __builtin_fmaf(A[r * ac + a], B[r * bc + b], s);
   out[(int64_t)(net0 + k) * ac * bc + e] = s;
+}
+
+// ---------------------------------------------------------------------------
+// grouped GEMM family on FP32 MFMA (v_mfma_f32_16x16x4_f32). MAGMA's
+// accumulation order (multimatmul.cu) is unknown and differs from any fixed
+// chain; results are compared with the sequential restatement within the
+// summation-order bound 2 n u sum|terms| (tests/test_gpu_kilonerf.py).
+// ---------------------------------------------------------------------------
+typedef float kn_f32x4 __attribute__((ext_vector_type(4)));
+constexpr int GG_ROWS = 64;                // rows per workgroup: 4 waves x 16
+constexpr int GG_MAX_IN = 120;             // K (padded to 4) held in LDS
+constexpr int GG_MAX_OUT = 64;             // N (padded to 16): 4 accumulator tiles per wave
+__host__ __device__ __forceinline__ int gg_wstride(int np) { return np % 32 == 0 ? np + 16 : np; }
+
+// out[r] = X[r] . W_net (+ bias_net), rows of network net0 + blockIdx.y, 64 per
+// workgroup (blockIdx.x). W_net and the X tile (one contiguous run of rows)
+// are staged in LDS; wave w owns tile rows 16w .. 16w+15: A = X (16 rows x 4
+// k), B = W (4 k x 16 columns), one accumulator per 16-column tile.
+__global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
+    int mode, const float* __restrict__ bias, const float* __restrict__ X,
+    const float* __restrict__ W, int out_f, int in_f, float* __restrict__ out, SegBatch sb,
+    int net0) {
+  extern __shared__ float gg_sm[];
+  const int k = blockIdx.y;
+  const int64_t r0 = sb.off[k], rows = sb.off[k + 1] - r0;
+  const int64_t t0 = (int64_t)blockIdx.x * GG_ROWS;
+  if (t0 >= rows) return;   // block-uniform
+  const int net = net0 + k;
+  const int kp = (in_f + 3) & ~3, np = (out_f + 15) & ~15;
+  const int ws = gg_wstride(np), xs = kp + 1;   // LDS row strides
+  float* Ws = gg_sm;                            // [kp][ws]
+  float* Xs = gg_sm + kp * ws;                  // [64][xs]
+  const float* w = W + (int64_t)net * out_f * in_f;
+  for (int i = threadIdx.x; i < kp * np; i += 256) {
+    const int kk = i / np, c = i - kk * np;
+    float v = 0.0f;
+    if (kk < in_f && c < out_f) v = mode == 2 ? w[(int64_t)c * in_f + kk] : w[(int64_t)kk * out_f + c];
+    Ws[kk * ws + c] = v;
+  }
+  const int64_t nrow = rows - t0 < GG_ROWS ? rows - t0 : GG_ROWS;
+  const float* x = X + (r0 + t0) * in_f;   // nrow * in_f contiguous floats
+  for (int i = threadIdx.x; i < GG_ROWS * kp; i += 256) {
+    const int rr = i / kp, kk = i - rr * kp;
+    Xs[rr * xs + kk] = (rr < nrow && kk < in_f) ? x[(int64_t)rr * in_f + kk] : 0.0f;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int nt = np / 16;
+  kn_f32x4 acc[GG_MAX_OUT / 16];
+#pragma unroll
+  for (int c = 0; c < GG_MAX_OUT / 16; ++c) acc[c] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* xa = Xs + (wave * 16 + l16) * xs + kq;
+  const float* wb = Ws + kq * ws + l16;
+  for (int k0 = 0; k0 < kp; k0 += 4) {
+    const float a = xa[k0];
+#pragma unroll
+    for (int c = 0; c < GG_MAX_OUT / 16; ++c)
+      if (c < nt) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[k0 * ws + 16 * c], acc[c], 0, 0, 0);
+  }
+  // lane holds rows 4 kq + i, column l16 of each 16-column tile
+#pragma unroll
+  for (int c = 0; c < GG_MAX_OUT / 16; ++c) {
+    const int col = 16 * c + l16;
+    if (c < nt && col < out_f) {
+      const float bb = mode == 0 ? bias[(int64_t)net * out_f + col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = wave * 16 + 4 * kq + i;
+        if (rr < nrow) out[(r0 + t0 + rr) * out_f + col] = mode == 0 ? acc[c][i] + bb : acc[c][i];
+      }
+    }
+  }
+}
+
+constexpr int AB_MAX_T = 4;   // 16-wide tiles per side (a_cols, b_cols <= 64)
+
+// out_net = A_net^T B_net ([ac][bc]) over the network's rows, one workgroup
+// per network: wave w takes row quads w, w+4, ...; A operand = A^T (16 a x
+// 4 rows), B operand = B (4 rows x 16 b); the 4 waves' partial tiles are
+// summed in LDS in wave order.
+__global__ __launch_bounds__(256) void kn_at_b_mfma_kernel(const float* __restrict__ A, int ac,
+                                                           const float* __restrict__ B, int bc,
+                                                           float* __restrict__ out, SegBatch sb,
+                                                           int net0) {
+  extern __shared__ float ab_sm[];
+  const int k = blockIdx.x;
+  const int64_t r0 = sb.off[k], r1 = sb.off[k + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int ta = (ac + 15) / 16, tb = (bc + 15) / 16;
+  kn_f32x4 acc[AB_MAX_T][AB_MAX_T];
+#pragma unroll
+  for (int i = 0; i < AB_MAX_T; ++i)
+#pragma unroll
+    for (int j = 0; j < AB_MAX_T; ++j) acc[i][j] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t rb = r0 + 4 * wave; rb < r1; rb += 16) {
+    const int64_t r = rb + kq;
+    const bool ok = r < r1;
+    float a[AB_MAX_T], b[AB_MAX_T];
+#pragma unroll
+    for (int i = 0; i < AB_MAX_T; ++i) {
+      const int ca = 16 * i + l16, cb = 16 * i + l16;
+      a[i] = (i < ta && ok && ca < ac) ? A[r * ac + ca] : 0.0f;
+      b[i] = (i < tb && ok && cb < bc) ? B[r * bc + cb] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < AB_MAX_T; ++i)
+#pragma unroll
+      for (int j = 0; j < AB_MAX_T; ++j)
+        if (i < ta && j < tb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+  // partial tile (i, j) of wave w at ab_sm[((w * ta + i) * tb + j) * 256 + 64 * e + lane]
+#pragma unroll
+  for (int i = 0; i < AB_MAX_T; ++i)
+#pragma unroll
+    for (int j = 0; j < AB_MAX_T; ++j)
+      if (i < ta && j < tb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ab_sm[((wave * ta + i) * tb + j) * 256 + 64 * e + lane] = acc[i][j][e];
+  __syncthreads();
+  const int per = ta * tb * 256;
+  float* o = out + (int64_t)(net0 + k) * ac * bc;
+  for (int idx = threadIdx.x; idx < per; idx += 256) {
+    const int tile = idx >> 8, e = (idx >> 6) & 3, ln = idx & 63;
+    const int i = tile / tb, j = tile - i * tb;
+    const int ra = 16 * i + 4 * (ln >> 4) + e, cbx = 16 * j + (ln & 15);
+    if (ra < ac && cbx < bc) {
+      float s = ab_sm[idx];
+      for (int w = 1; w < 4; ++w) s = s + ab_sm[w * per + idx];
+      o[(int64_t)ra * bc + cbx] = s;
+    }
+  }
+}
+
+// out_net[c] = sum over the network's rows of M[r][c]: one workgroup per
+// (network, 32 columns); 8 row phases per column (loads of a phase unrolled so
+// several are in flight) summed in LDS in phase order.
+constexpr int RSB_COLS = 32, RSB_PH = 8;
+__global__ __launch_bounds__(256) void kn_row_sum_blk_kernel(const float* __restrict__ M,
+                                                             int64_t cols, float* __restrict__ out,
+                                                             SegBatch sb, int net0) {
+  __shared__ float part[RSB_PH][RSB_COLS];
+  const int k = blockIdx.y;
+  const int64_t r0 = sb.off[k], r1 = sb.off[k + 1];
+  const int cl = threadIdx.x % RSB_COLS, ph = threadIdx.x / RSB_COLS;
+  const int64_t c = (int64_t)blockIdx.x * RSB_COLS + cl;
+  float s = 0.0f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int64_t r = r0 + ph; r < r1; r += RSB_PH) s = s + M[r * cols + c];
+  }
+  part[ph][cl] = s;
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    float t = part[0][cl];
+#pragma unroll
+    for (int p = 1; p < RSB_PH; ++p) t = t + part[p][cl];
+    out[(int64_t)(net0 + k) * cols + c] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -751,6 +902,14 @@ int kn_multimatmul_grouped(int handle, int mode, const float* biases, const floa
                "kn_multimatmul_grouped: bad feature sizes");
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t mr) {
     if (mr == 0) return 0;
+    if (in_f <= GG_MAX_IN && out_f <= GG_MAX_OUT) {
+      const int kp = ((int)in_f + 3) & ~3, np = ((int)out_f + 15) & ~15;
+      const size_t lds = (size_t)(kp * gg_wstride(np) + GG_ROWS * (kp + 1)) * sizeof(float);
+      hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel, dim3((unsigned)cdiv(mr, GG_ROWS), sb.count),
+                         dim3(256), lds, as_stream(stream), mode, biases, X, W, (int)out_f,
+                         (int)in_f, out, sb, net0);
+      return check_launch("kn_grouped_gemm_mfma_kernel");
+    }
     hipLaunchKernelGGL(kn_grouped_gemm_kernel, dim3((unsigned)cdiv(mr * out_f, 256), sb.count),
                        dim3(256), 0, as_stream(stream), mode, biases, X, W, (int)out_f, (int)in_f,
                        out, sb, net0);
@@ -763,9 +922,9 @@ int kn_multi_row_sum_reduction(const float* M, int64_t cols, const int64_t* bspn
   NERF_REQUIRE(M && bspn && out && cols > 0 && num_networks >= 0,
                "kn_multi_row_sum_reduction: bad argument");
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t) {
-    hipLaunchKernelGGL(kn_row_sum_kernel, dim3((unsigned)cdiv(cols, 256), sb.count), dim3(256), 0,
-                       as_stream(stream), M, cols, out, sb, net0);
-    return check_launch("kn_row_sum_kernel");
+    hipLaunchKernelGGL(kn_row_sum_blk_kernel, dim3((unsigned)cdiv(cols, RSB_COLS), sb.count), dim3(256),
+                       0, as_stream(stream), M, cols, out, sb, net0);
+    return check_launch("kn_row_sum_blk_kernel");
   });
 }
 
@@ -775,6 +934,12 @@ int kn_multimatmul_A_transposed(const float* A, int64_t a_cols, const float* B, 
   NERF_REQUIRE(A && B && bspn && out && a_cols > 0 && b_cols > 0 && num_networks >= 0,
                "kn_multimatmul_A_transposed: bad argument");
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t) {
+    if (a_cols <= 16 * AB_MAX_T && b_cols <= 16 * AB_MAX_T) {
+      const size_t lds = 4 * cdiv(a_cols, 16) * cdiv(b_cols, 16) * 256 * sizeof(float);
+      hipLaunchKernelGGL(kn_at_b_mfma_kernel, dim3((unsigned)sb.count), dim3(256), lds,
+                         as_stream(stream), A, (int)a_cols, B, (int)b_cols, out, sb, net0);
+      return check_launch("kn_at_b_mfma_kernel");
+    }
     hipLaunchKernelGGL(kn_at_b_kernel, dim3((unsigned)cdiv(a_cols * b_cols, 256), sb.count),
                        dim3(256), 0, as_stream(stream), A, a_cols, B, b_cols, out, sb, net0);
     return check_launch("kn_at_b_kernel");

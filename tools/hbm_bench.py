@@ -121,6 +121,30 @@ def main():
     src4 = torch.rand(ng, 4, device=dev, generator=g)
     t = timed(lambda: kc.scatter_int32_float4(mp_, src4))
     report("kn_scatter_int32_float4 (random map)", ng * 36, t, "map 4 + in 16 + out 16 B/element")
+    del mp_, src, src4
+
+    # KiloNeRF grouped GEMMs (multimatmul.cu): 4096 networks, ragged 0..511 rows
+    nets, hd, inf = 4096, 32, 63
+    bspn = torch.randint(0, 512, (nets,), generator=torch.Generator().manual_seed(1))
+    rows = int(bspn.sum())
+    X = torch.randn(rows, inf, device=dev, generator=g)
+    Wg = torch.randn(nets * hd * inf, device=dev, generator=g) * 0.1
+    bg = torch.randn(nets, hd, device=dev, generator=g)
+    h = kc.init_multimatmul_magma_grouped(nets, hd, inf, [])
+    t = timed(lambda: kc.multimatmul_magma_grouped_static(bg, X, Wg, hd, inf, bspn, 128, 256, [], h))
+    kc.deinit_multimatmul_magma_grouped(h)
+    report(f"kn_multimatmul_grouped {nets} nets {inf}->{hd} ({rows} rows)",
+           rows * (inf + hd) * 4 + nets * hd * (inf + 1) * 4, t,
+           "X 4 B/in + out 4 B/out per row + W and bias once (FP32 MFMA kernel; "
+           f"{2 * rows * inf * hd / t / 1e12:.2f} TFLOP/s)")
+    Bm = torch.randn(rows, inf, device=dev, generator=g)
+    Am = torch.randn(rows, hd, device=dev, generator=g)
+    t = timed(lambda: kc.multimatmul_A_transposed(Am, Bm, bspn))
+    report(f"kn_multimatmul_A_transposed {nets} nets {hd}x{inf}", rows * (inf + hd) * 4
+           + nets * hd * inf * 4, t, "A, B 4 B per element once + out")
+    t = timed(lambda: kc.multi_row_sum_reduction(Am, bspn))
+    report(f"kn_multi_row_sum_reduction {nets} nets x{hd}", rows * hd * 4 + nets * hd * 4, t,
+           "M 4 B per element once + out")
 
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:
