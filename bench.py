@@ -363,6 +363,10 @@ def roofline(precision, timer, elapsed, world, H, W, pmc_workload=True):
             if mlp_ms > 0 else 0.0
         kernel, achieved, peak, unit = ("mlp_x3_kernel", exec_tflops, FP16_MFMA_PEAK_TFLOPS,
                                         "TFLOP/s (FP16 MFMA executed, 3 per FP32 product)")
+    # weight bytes the kernel stages L2 -> LDS: every 128-sample tile streams the
+    # whole packed network (65 x 32 KiB x3 slices; 73 x 32 KiB FP32)
+    slices = 65 if precision != "fp32" else 73
+    staged = sum(-(-int(s) // 128) for _, _, s, _ in timer) * slices * 32768
     return {"bound": "mfma", "kernel": kernel,
             "achieved": achieved, "peak": peak, "unit": unit,
             "frac": achieved / peak,
@@ -371,6 +375,8 @@ def roofline(precision, timer, elapsed, world, H, W, pmc_workload=True):
             "traffic": pmc_traffic(H, W, kernel) if pmc_workload else None,
             "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
             "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
+            "lds_staged_bytes_per_launch": staged / max(1, n_launch),
+            "lds_staging_TBps": staged / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0,
             "launches": n_launch,
             "avg_launch_ms": mlp_ms / max(1, n_launch),
             "flop_per_sample": NerfPipeline.MLP_FLOP_PER_SAMPLE,
