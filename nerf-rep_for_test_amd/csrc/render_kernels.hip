@@ -97,6 +97,20 @@ __device__ __forceinline__ void maps_add(Maps& m, float w, const float4& v, floa
   m.a += w;
 }
 
+// sigmoid on the hardware exp2 / reciprocal (each ~1 ulp): the colour maps move
+// by < 4e-7, inside the 1e-6 the kernels are tested to; alpha and the weights,
+// which feed _sample_fine's searchsorted, keep the accurate expf
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+__device__ __forceinline__ void maps_add_fast(Maps& m, float w, const float4& v, float z) {
+  m.r += w * sigmoid_fast(v.x);
+  m.g += w * sigmoid_fast(v.y);
+  m.b += w * sigmoid_fast(v.z);
+  m.d += w * z;
+  m.a += w;
+}
+
 __device__ __forceinline__ Maps maps_reduce(Maps m) {
   return Maps{wave_sum(m.r), wave_sum(m.g), wave_sum(m.b), wave_sum(m.d), wave_sum(m.a)};
 }
@@ -173,6 +187,86 @@ __global__ __launch_bounds__(64 * COMP_WAVES) void composite_kernel(
   composite_ray<false>(raw + ray * S, z + ray * z_stride, nd, S, lane, 0.f,
                        wout ? wout + ray * S : nullptr, full, cut, first);
   if (lane == 0) maps_store(full, ray, white, rgb, disp, acc, depth);
+}
+
+// 16 lanes per ray, 4 rays per wave (S <= 256): lane t holds samples t + 16k,
+// k < C, so every load instruction reads 16 consecutive float4 of each of 4
+// rays. The transmittance is C interleaved 16-lane product scans in double
+// (one per row of 16 consecutive samples, independent, so their shuffles are
+// in flight together), each row then scaled by the product of the rows before
+// it; the map sums are per-lane then a 16-lane butterfly. No LDS.
+constexpr int COMP16_RPB = 16;   // rays per 256-thread block
+
+template <int C>
+__global__ __launch_bounds__(256) void composite16_kernel(
+    const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
+    const float* __restrict__ rays_d, int64_t n, int S, int white, float* __restrict__ rgb,
+    float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ depth,
+    float* __restrict__ wout) {
+  const int lane = threadIdx.x & 63, t = lane & 15;
+  const int64_t ray0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+  if (ray0 >= n) return;   // wave-uniform
+  const int64_t ray = ray0 + (lane >> 4);
+  const bool live = ray < n;          // rays past n (last wave) recompute ray n-1, store nothing
+  const int64_t rr = live ? ray : n - 1;
+  const float nd = torch_norm3(rays_d[rr * 3], rays_d[rr * 3 + 1], rays_d[rr * 3 + 2]);
+  const float4* rp = raw + rr * S;
+  const float* zr = z + rr * z_stride;
+  float4 v[C];
+  float zs[C], zn[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    const int s = t + 16 * k;
+    v[k] = s < S ? rp[s] : make_float4(0.f, 0.f, 0.f, 0.f);
+    zs[k] = s < S ? zr[s] : 0.0f;
+    zn[k] = s + 1 < S ? zr[s + 1] : 0.0f;
+  }
+  float a[C];
+  double p[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    const int s = t + 16 * k;
+    const float dist = ((s < S - 1) ? (zn[k] - zs[k]) : 1e10f) * nd;   // VR:290-292
+    a[k] = s < S ? 1.0f - expf((-fmaxf(v[k].w, 0.0f)) * dist) : 0.0f;   // VR:288
+    p[k] = s < S ? (double)((1.0f - a[k]) + 1e-10f) : 1.0;
+  }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    double q[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) q[k] = __shfl_up(p[k], o, 16);
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+      if (t >= o) p[k] *= q[k];
+  }
+  double ex[C], tot[C];
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    ex[k] = __shfl_up(p[k], 1, 16);
+    tot[k] = __shfl(p[k], (lane & ~15) | 15);
+  }
+  Maps m{0, 0, 0, 0, 0};
+  double carry = 1.0;
+#pragma unroll
+  for (int k = 0; k < C; ++k) {
+    const int s = t + 16 * k;
+    const float T = (float)(carry * (t == 0 ? 1.0 : ex[k]));
+    carry = carry * tot[k];
+    const float w = a[k] * T;
+    if (s < S) {
+      if (wout && live) wout[rr * S + s] = w;
+      maps_add_fast(m, w, v[k], zs[k]);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    m.r += __shfl_xor(m.r, o, 16);
+    m.g += __shfl_xor(m.g, o, 16);
+    m.b += __shfl_xor(m.b, o, 16);
+    m.d += __shfl_xor(m.d, o, 16);
+    m.a += __shfl_xor(m.a, o, 16);
+  }
+  if (t == 0 && live) maps_store(m, ray, white, rgb, disp, acc, depth);
 }
 
 // ERT (VR:1089-1133): if any ray of the 2048-ray chunk has T < thr, every ray's
@@ -710,6 +804,20 @@ int nerf_composite(const float* raw, const float* z, int64_t z_stride, const flo
                "nerf_composite: null pointer");
   NERF_REQUIRE(n >= 0 && S >= 2 && S < 1024, "nerf_composite: S must be in [2, 1024)");
   if (n == 0) return 0;
+  if (S <= 256) {
+    const int c = (S + 15) / 16;
+    const dim3 grid((unsigned)cdiv(n, COMP16_RPB)), block(256);
+#define NERF_COMP16(CC)                                                                        \
+  hipLaunchKernelGGL((composite16_kernel<CC>), grid, block, 0, as_stream(stream),              \
+                     (const float4*)raw, z, z_stride, rays_d, n, S, white_bkgd, rgb, disp, acc, \
+                     depth, weights)
+    if (c <= 4) NERF_COMP16(4);
+    else if (c <= 8) NERF_COMP16(8);
+    else if (c <= 12) NERF_COMP16(12);
+    else NERF_COMP16(16);
+#undef NERF_COMP16
+    return check_launch("composite16_kernel");
+  }
   hipLaunchKernelGGL(composite_kernel, dim3((unsigned)cdiv(n, COMP_WAVES)), dim3(64 * COMP_WAVES), 0,
                      as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S,
                      white_bkgd, rgb, disp, acc, depth, weights);

@@ -277,7 +277,9 @@ class NerfTrainer:
                                         lr=torch.tensor(lr, device=self.device), eps=1e-8,
                                         weight_decay=0.0, capturable=True, foreach=True)
         else:
-            self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0)
+            # one fused multi-tensor Adam kernel per step on the GPU
+            self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0,
+                                        fused=self.device.type == "cuda")
         self._graphs = {}
         self._warm = {}
         self.z_base = coarse_depth_table(near, far, self.N_samples, False).to(self.device)
