@@ -46,6 +46,7 @@ FP16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS   # dense FP16/BF16 MFMA (1/1
 # products, x2 FLOP. The algorithmic count (the reference's FLOPs) stays
 # NerfPipeline.MLP_FLOP_PER_SAMPLE = 1 186 816.
 X3_EXEC_FLOP_PER_SAMPLE = 2 * 3 * 528384
+HBM_PEAK_BPS = 8.0e12          # MI355X_MICROARCH.md
 METRIC = "Mrays/s + ms/frame, lego 800x800 (64c+128f); PSNR vs ref"
 
 
@@ -163,6 +164,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         pipe.timer = []
+        pipe.stage_timer = []
         pipe.ert_stats = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -176,8 +178,10 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         timer, pipe.timer = pipe.timer, None
-        return pipe, elapsed, roofline(precision, timer, elapsed, world, H, W,
-                                       pmc_workload=world == 1 and not c4)
+        stages, pipe.stage_timer = pipe.stage_timer, None
+        roof = roofline(precision, timer, elapsed, world, H, W, pmc_workload=world == 1 and not c4)
+        roof["byte_kernels"] = byte_kernels(stages, args.steps)
+        return pipe, elapsed, roof
 
     pipe, elapsed, roof = measure(args.precision)
     rays = H * W * args.steps
@@ -381,6 +385,23 @@ def roofline(precision, timer, elapsed, world, H, W, pmc_workload=True):
             "avg_launch_ms": mlp_ms / max(1, n_launch),
             "flop_per_sample": NerfPipeline.MLP_FLOP_PER_SAMPLE,
             "mlp_share_of_step": (mlp_ms / world) / (elapsed * 1e3) if world == 1 else None}
+
+
+def byte_kernels(stages, steps):
+    """The HBM-bound stages of the frame (compositing = the reference's
+    integrate, fine sampling), timed live by HIP events on their launch stream
+    over the timed frames: algorithmic bytes / time against the 8 TB/s roof."""
+    out = {}
+    for name, e0, e1, nb in stages:
+        d = out.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0})
+        d["launches"] += 1
+        d["ms"] += e0.elapsed_time(e1)
+        d["bytes"] += nb
+    for d in out.values():
+        d["ms_per_frame"] = d["ms"] / max(1, steps)
+        d["GBps"] = d["bytes"] / (d["ms"] * 1e-3) / 1e9 if d["ms"] > 0 else 0.0
+        d["frac_hbm"] = d["GBps"] * 1e9 / HBM_PEAK_BPS
+    return out
 
 
 def pmc_traffic(H, W, kernel="mlp_fused_kernel"):

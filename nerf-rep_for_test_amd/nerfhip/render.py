@@ -77,6 +77,7 @@ class NerfPipeline:
         self.coarse = None
         self.fine = None
         self.timer = None         # list -> (start event, end event, samples, bytes) per MLP launch
+        self.stage_timer = None   # list -> (kernel, start event, end event, algorithmic bytes)
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, params, coarse_prefix="model", fine_prefix="model_fine"):
@@ -158,6 +159,20 @@ class NerfPipeline:
         self.ert_stats.append((counts, n, S))
         return raw
 
+    def _timed(self, name, nbytes, fn):
+        """Run fn(); with stage_timer set, bracket it by HIP events on the launch
+        stream and record (name, events, algorithmic bytes)."""
+        t = self.stage_timer
+        if t is None:
+            return fn()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        t.append((name, e0, e1, nbytes))
+        return r
+
     def composite(self, raw, z, z_stride, rays_d, n, S, out, off, need_weights=True):
         """Writes rgb/disp/acc/depth rows [off, off+n) of `out`; returns the weights
         [n, S] (or None when not needed: the kernel then skips writing them)."""
@@ -169,8 +184,9 @@ class NerfPipeline:
                 _lib.stream_of(self.device))
         if self.enable_ert:
             call("nerf_composite_ert", *args, self.ert_threshold, REF_CHUNK, *tail)
-        else:
-            call("nerf_composite", *args, *tail)
+        else:   # raw 16 B/sample, z, rays_d 12 B/ray, maps 24 B/ray, weights 4 B/sample
+            nb = n * S * 16 + (n * S if z_stride else S) * 4 + n * 36 + (n * S * 4 if w is not None else 0)
+            self._timed("composite", nb, lambda: call("nerf_composite", *args, *tail))
         return w
 
     # ------------------------------------------------------------------ rays
@@ -222,7 +238,10 @@ class NerfPipeline:
                     uu, us = self.u_eval, 0
                 else:
                     uu, us = u[p:p + m], NI
-                call("nerf_sample_fine", ptr(z), zs, ptr(w), ptr(uu), us, m, S, NI, ptr(zall), st)
+                nb = m * S * 4 + (m * S if zs else S) * 4 + (m * NI if us else NI) * 4 \
+                    + m * (S + NI) * 4   # weights, z, u in; merged depths out
+                self._timed("sample_fine", nb, lambda: call(
+                    "nerf_sample_fine", ptr(z), zs, ptr(w), ptr(uu), us, m, S, NI, ptr(zall), st))
                 del raw, w
                 raw_f = self._pass_mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
                 w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p,
