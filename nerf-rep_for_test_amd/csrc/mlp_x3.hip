@@ -397,6 +397,9 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const int wave = tid >> 6;
   Ring R{ring, slices, wave, lane};
 
+#if defined(MLP_X3_SKEW)   // timing experiment: workgroups of one XCD start staggered
+  for (int i = 0; i < (int)((blockIdx.x >> 3) & 7) * MLP_X3_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   for (int t = 0; t < kX3DmaAhead; ++t)
     stage_slice(make_dma(slices, t, R.buf(t), wave, lane));   // all 8 waves, 4 pieces each
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)

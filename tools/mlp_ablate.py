@@ -56,7 +56,10 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             # the loading half = waves 4-7, alone and with priority for waves 0-3
             "x3_ldhi": ["-DMLP_X3_LOADER_HI=1"],
             "x3_ldhi_prio_lo": ["-DMLP_X3_LOADER_HI=1", "-DMLP_X3_PRIO=2"],
-            "x3_ilv1": ["-DMLP_X3_ILV=1"], "x3_ilv3": ["-DMLP_X3_ILV=3"]}
+            "x3_ilv1": ["-DMLP_X3_ILV=1"], "x3_ilv3": ["-DMLP_X3_ILV=3"],
+            # workgroups of an XCD start staggered by k * N s_sleep(127) (k = 0..7)
+            "x3_skew1": ["-DMLP_X3_SKEW=1"], "x3_skew2": ["-DMLP_X3_SKEW=2"],
+            "x3_skew3": ["-DMLP_X3_SKEW=3"]}
 
 
 def is_x3(v):
