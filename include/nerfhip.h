@@ -109,6 +109,9 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
  * d_weights [n][S] (rows 0 and S-1 zero) from g_zall [n][S + n_imp]. z [n][S],
  * weights [n][S], u [n][n_imp] as given to the forward. S <= 130,
  * n_imp <= 256. */
+/* nerf_sum_partials: out[i] = sum_{c=0}^{C-1} part[c * n + i], summed in c
+ *   order (the weight-gradient split-K partials of nerf_x3_wgrad). */
+int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream);
 int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
                         const float* g_zall, int64_t n, int S, int n_imp,
                         float* d_weights, nerf_stream_t stream);
@@ -152,9 +155,43 @@ int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_
                   const float* bias, const float* B, int64_t ldb, const float* mask,
                   int64_t ldm, const float* ru, const float* rw, int relu, float* C,
                   int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream);
+/* nerf_x3_layer_bits: nerf_x3_layer with the ReLU mask carried as bits.
+ *   relu_bits (nullable, needs relu) receives bit (C[m][p] > 0) of every output
+ *   element; mask_bits (nullable, instead of mask) multiplies C by such a bit.
+ *   Layout: u16 word ((p / 128 * 8 + p % 128 / 16) * m_tiles / 4 + m / 64) * 64
+ *   + (p % 16) + 16 * (m % 16 / 4), bit 4 * (m % 64 / 16) + m % 4: the layer
+ *   kernel's own lane order, so producer and consumer have the same m_tiles
+ *   (16: the 256-wide layers); ceil(P / 128) * 128 * m_tiles words. 32 B per
+ *   sample and 256-wide layer, where the FP32 mask is 1 KiB. */
+int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
+                       const float* bias, const float* B, int64_t ldb, const float* mask,
+                       int64_t ldm, const float* ru, const float* rw, int relu, float* C,
+                       int64_t ldc, int64_t P, float* amax_out, unsigned short* relu_bits,
+                       const unsigned short* mask_bits, nerf_stream_t stream);
 int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                   int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
                   float* part, float* bias_part, nerf_stream_t stream);
+/* nerf_x3_wgrad_batch: n (<= 16) weight gradients of one backward in ONE
+ *   launch, each split over `chunks` sample subsets (instead of ~256 per
+ *   nerf_x3_wgrad call): subset c of descriptor k writes part + c * ldpart
+ *   ([M][N]) and bias_part + c * ldbias ([M], optional); the same definitions
+ *   as nerf_x3_wgrad. Operands must be aligned (P % 32 == 0, lda / ldb % 4 ==
+ *   0, 16-byte aligned, < 2 GiB). descs is a host array (passed by value). */
+typedef struct NerfWgradDesc {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  int64_t P;
+  const float* amax_a;
+  const float* amax_b;
+  float* part;
+  int64_t ldpart;
+  float* bias_part;
+  int64_t ldbias;
+  int M, N;
+} NerfWgradDesc;
+int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
 /* nerf_freq_encode_fm: the frequency encoding of freq.py:7-32 (reference
  *   embed_fn / embeddirs_fn, encoding/__init__.py:7-18), written feature-major
  *   for the training MLP: out[j * ldo + p] for the 3 + 6 * n_freq columns of

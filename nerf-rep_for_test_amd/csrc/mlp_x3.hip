@@ -629,7 +629,15 @@ __device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op
 // rest of the tile computes. Each tile ends with vmcnt(0): within a tile the
 // counted wait before a slice barrier then only counts that tile's operations.
 // epilogue terms, a compile-time set (no per-element branches or waits)
-enum : int { kEpiBias = 1, kEpiRelu = 2, kEpiMask = 4, kEpiRank1 = 8 };
+// kEpiMaskBits: the mask as one bit per element (written by a forward launch
+// with kEpiOutBits: bit (C > 0) of its ReLU output) instead of an FP32 tensor,
+// in this kernel's own lane layout (so the consumer has the producer's MT):
+// per block of 4 tiles a lane keeps the 16 bits of its sample (tile * 128 +
+// wave * 16 + (lane & 15)) and rows 16 (u0 + t) + 4 (lane >> 4) + r, bit
+// 4 t + r, as one u16 at ((tile * 8 + wave) * MT / 4 + u0 / 4) * 64 + lane:
+// 32 B per sample and 256-row layer instead of the 1 KiB of the FP32 mask.
+enum : int { kEpiBias = 1, kEpiRelu = 2, kEpiMask = 4, kEpiRank1 = 8, kEpiMaskBits = 16,
+             kEpiOutBits = 32 };
 
 __device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n uniform
   switch (n) {
@@ -653,7 +661,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
     const float* __restrict__ bias, const float* __restrict__ B, int64_t ldb,
     const float* __restrict__ mask, int64_t ldm, const float* __restrict__ ru,
     const float* __restrict__ rw, float* __restrict__ C, int64_t ldc, int64_t P,
-    float* __restrict__ amax_out) {
+    float* __restrict__ amax_out, unsigned short* __restrict__ bits_out,
+    const unsigned short* __restrict__ bits_in) {
   constexpr int kPieces = 2 * MT;          // 1-KiB LDS-DMA pieces per slice
   constexpr int kSliceU4 = kPieces * 64;
   constexpr int kPpw = kPieces / 8;        // pieces per wave
@@ -778,6 +787,10 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
 #pragma unroll
     for (int u0 = 0; u0 < MT; u0 += 4) {
       float v[4][4], mk[4][4];
+      // this block's 16 mask bits of this lane (u16 word)
+      const int64_t wb = (((tile * 8 + wave) * MT + u0) / 4) * 64 + lane;
+      unsigned mbits = 0u;
+      if constexpr ((EPI & kEpiMaskBits) != 0) mbits = bits_in[wb];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -796,7 +809,19 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
         for (int r = 0; r < 4; ++r) {
           if constexpr ((EPI & kEpiRelu) != 0) v[t][r] = fmaxf(v[t][r], 0.0f);
           if constexpr ((EPI & kEpiMask) != 0) v[t][r] = mk[t][r] > 0.0f ? v[t][r] : 0.0f;
+          if constexpr ((EPI & kEpiMaskBits) != 0)
+            v[t][r] = ((mbits >> (4 * t + r)) & 1u) ? v[t][r] : 0.0f;
         }
+      if constexpr ((EPI & kEpiOutBits) != 0) {
+        // bit 4 t + r = (v > 0): post-ReLU v >= 0, so min(bits(v), 1)
+        unsigned mine = 0u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            mine |= min(__float_as_uint(v[t][r]), 1u) << (4 * t + r);
+        if (valid) bits_out[wb] = (unsigned short)mine;
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -980,16 +1005,18 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 // 8 (l >> 4) + 4h .. +3, so the two halves read by lane l are one MFMA
 // fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past M / N read 0
 // (offset past num_records). Bias sums from the A fragments (waves nb = 0).
-__global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
-    const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
-    int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
-    float* __restrict__ part, float* __restrict__ bias_part) {
-  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
+// The body for output tile (mtile, ntile) and K subset z of Z; subset z's
+// partials go to part + z * ldpart ([M][N]) and bias_part + z * ldbias ([M]).
+__device__ __forceinline__ void wgrad_dma_body(
+    uint4 (&stg)[2][64 * 64], const float* __restrict__ A, int64_t lda, int M,
+    const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float* __restrict__ amax_a,
+    const float* __restrict__ amax_b, float* __restrict__ part, int64_t ldpart,
+    float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
-  const int m0 = blockIdx.x * kWgTile, n0 = blockIdx.y * kWgTile;
-  const int64_t pb = (int64_t)blockIdx.z * 32, kstride = (int64_t)gridDim.z * 32;
+  const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
+  const int64_t pb = (int64_t)z * 32, kstride = (int64_t)Z * 32;
   const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
 
@@ -1087,19 +1114,19 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
       }
     }
   }
-  if (bias_part && blockIdx.y == 0 && nb == 0 && busy) {
+  if (bias_part && ntile == 0 && nb == 0 && busy) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // row 16 (4 mb + i) + (l & 15): lanes l, l^16, l^32, l^48
       float r = rs4[i];
       r += __shfl_xor(r, 16);
       r += __shfl_xor(r, 32);
       const int row = m0 + 16 * (4 * mb + i) + lane;
-      if (lane < 16 && row < M) bias_part[(int64_t)blockIdx.z * M + row] = r;
+      if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
     }
   }
   if (!busy) return;
   const float inv = ldexpf(1.0f, -(ea + eb));
-  float* out = part + (int64_t)blockIdx.z * M * N;
+  float* out = part + (int64_t)z * ldpart;
   const int g4 = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1111,6 +1138,39 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
         const int n = n0 + 128 * nb + 16 * j + (lane & 15);
         if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][r] * inv;
       }
+}
+
+__global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
+    const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
+    int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
+    float* __restrict__ part, float* __restrict__ bias_part) {
+  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
+  wgrad_dma_body(stg, A, lda, M, B, ldb, N, P, amax_a, amax_b, part, (int64_t)M * N, bias_part,
+                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z);
+}
+
+// Several weight gradients in one launch (the whole backward of a network):
+// workgroup w -> (descriptor, output tile, K subset z of Z) with the Z subsets
+// of a tile adjacent, so every layer is split Z ways instead of ~256 and its
+// partials are Z x M x N instead of 256 x M x N (nerf_x3_wgrad_batch).
+constexpr int kWgBatchMax = 16;
+struct WgradBatch {
+  NerfWgradDesc d[kWgBatchMax];
+  int tiles_end[kWgBatchMax];   // prefix sums of mtiles * ntiles
+  int n, Z;
+};
+
+__global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const WgradBatch bt) {
+  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
+  const int z = (int)(blockIdx.x % (unsigned)bt.Z);
+  int tile = (int)(blockIdx.x / (unsigned)bt.Z);
+  int k = 0;
+  while (k + 1 < bt.n && tile >= bt.tiles_end[k]) ++k;
+  if (k > 0) tile -= bt.tiles_end[k - 1];
+  const NerfWgradDesc& d = bt.d[k];
+  const int mt = (d.M + kWgTile - 1) / kWgTile;
+  wgrad_dma_body(stg, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, d.amax_a, d.amax_b, d.part,
+                 d.ldpart, d.bias_part, d.ldbias, tile % mt, tile / mt, z, bt.Z);
 }
 
 
@@ -1251,13 +1311,14 @@ template <int MT, int NK, int EPI>
 static int launch_layer(const float* w, const int* sw, const float* bias, const float* B,
                         int64_t ldb, const float* mask, int64_t ldm, const float* ru,
                         const float* rw, float* C, int64_t ldc, int64_t P, float* amax_out,
+                        unsigned short* bits_out, const unsigned short* bits_in,
                         nerf_stream_t stream) {
   // persistent: at most one workgroup per CU (the ring takes 64-128 KiB of LDS)
   const int64_t tiles = cdiv(P, kTrainTile);
   const int n_cu = stream_cu_count(stream);
   hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)(tiles < n_cu ? tiles : n_cu)),
                      dim3(kTrainThreads), 0, as_stream(stream), (const uint4*)w, sw, bias, B,
-                     ldb, mask, ldm, ru, rw, C, ldc, P, amax_out);
+                     ldb, mask, ldm, ru, rw, C, ldc, P, amax_out, bits_out, bits_in);
   return check_launch("x3_layer_kernel");
 }
 
@@ -1265,7 +1326,21 @@ extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_ti
                              const float* bias, const float* B, int64_t ldb, const float* mask,
                              int64_t ldm, const float* ru, const float* rw, int relu, float* C,
                              int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream) {
+  return nerf_x3_layer_bits(w_packed, w_scale, m_tiles, k_steps, bias, B, ldb, mask, ldm, ru, rw,
+                            relu, C, ldc, P, amax_out, nullptr, nullptr, stream);
+}
+
+extern "C" int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int m_tiles,
+                                  int k_steps, const float* bias, const float* B, int64_t ldb,
+                                  const float* mask, int64_t ldm, const float* ru, const float* rw,
+                                  int relu, float* C, int64_t ldc, int64_t P, float* amax_out,
+                                  unsigned short* relu_bits, const unsigned short* mask_bits,
+                                  nerf_stream_t stream) {
   NERF_REQUIRE(w_packed && w_scale && B && C, "nerf_x3_layer: null pointer");
+  NERF_REQUIRE(!(mask && mask_bits), "nerf_x3_layer: mask and mask_bits are exclusive");
+  NERF_REQUIRE(!relu_bits || relu, "nerf_x3_layer: relu_bits needs relu");
+  NERF_REQUIRE((((uintptr_t)relu_bits) | ((uintptr_t)mask_bits)) % 2 == 0,
+               "nerf_x3_layer: bit words must be 2-byte aligned");
   NERF_REQUIRE((ru == nullptr) == (rw == nullptr), "nerf_x3_layer: ru and rw go together");
   NERF_REQUIRE(P >= 0 && ldb >= P && ldc >= P && (!mask || ldm >= P), "nerf_x3_layer: bad size");
   NERF_REQUIRE(((uintptr_t)w_packed & 15) == 0, "nerf_x3_layer: packed W must be 16-byte aligned");
@@ -1275,11 +1350,12 @@ extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_ti
                "nerf_x3_layer: an operand spans 2 GiB or more (32-bit buffer offsets)");
   if (P == 0) return 0;
   const int epi = (bias ? kEpiBias : 0) | (relu ? kEpiRelu : 0) | (mask ? kEpiMask : 0) |
-                  (ru ? kEpiRank1 : 0);
+                  (ru ? kEpiRank1 : 0) | (mask_bits ? kEpiMaskBits : 0) |
+                  (relu_bits ? kEpiOutBits : 0);
 #define NERF_LAYER_CASE(MT, NK, EPI)                                                          \
   if (m_tiles == MT && k_steps == NK && epi == (EPI))                                         \
     return launch_layer<MT, NK, (EPI)>(w_packed, w_scale, bias, B, ldb, mask, ldm, ru, rw, C, \
-                                       ldc, P, amax_out, stream);
+                                       ldc, P, amax_out, relu_bits, mask_bits, stream);
   // forward layers (bias + ReLU; the feature layer without ReLU)
   NERF_LAYER_CASE(16, 2, kEpiBias | kEpiRelu) NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu)
   NERF_LAYER_CASE(16, 10, kEpiBias | kEpiRelu) NERF_LAYER_CASE(8, 9, kEpiBias | kEpiRelu)
@@ -1287,10 +1363,23 @@ extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_ti
   // backward layers (ReLU mask; + the alpha head's rank-1 term into d h7)
   NERF_LAYER_CASE(16, 4, 0) NERF_LAYER_CASE(16, 8, kEpiMask)
   NERF_LAYER_CASE(16, 8, kEpiMask | kEpiRank1) NERF_LAYER_CASE(4, 8, 0)
+  // the training MLP's mask path: forward layers write their ReLU bits, the
+  // dgrad layers read them (32 B per sample and layer instead of 1 KiB)
+  NERF_LAYER_CASE(16, 2, kEpiBias | kEpiRelu | kEpiOutBits)
+  NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiOutBits)
+  NERF_LAYER_CASE(16, 10, kEpiBias | kEpiRelu | kEpiOutBits)
+  NERF_LAYER_CASE(16, 8, kEpiMaskBits) NERF_LAYER_CASE(16, 8, kEpiMaskBits | kEpiRank1)
   // every term at once (tests)
   NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiMask | kEpiRank1)
 #undef NERF_LAYER_CASE
   return fail(NERF_E_UNSUPPORTED, "nerf_x3_layer: unsupported (m_tiles, k_steps, epilogue)");
+}
+
+static bool wgrad_dma_ok(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
+                         int64_t P) {
+  return P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+         ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
+         (int64_t)M * lda * 4 < ((int64_t)1 << 31) && (int64_t)N * ldb * 4 < ((int64_t)1 << 31);
 }
 
 extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb,
@@ -1304,9 +1393,7 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
   if (chunks == 0) return 0;
   NERF_REQUIRE(chunks < 65536, "nerf_x3_wgrad: too many chunks");
   const dim3 grid((unsigned)cdiv(M, kWgTile), (unsigned)cdiv(N, kWgTile), (unsigned)chunks);
-  const bool dma = P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
-                   ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
-                   (int64_t)M * lda * 4 < ((int64_t)1 << 31) && (int64_t)N * ldb * 4 < ((int64_t)1 << 31);
+  const bool dma = wgrad_dma_ok(A, lda, M, B, ldb, N, P);
   if (dma) {
     hipLaunchKernelGGL(x3_wgrad_dma_kernel, grid, dim3(kTrainThreads), 0, as_stream(stream), A,
                        lda, M, B, ldb, N, P, amax_a, amax_b, part, bias_part);
@@ -1315,6 +1402,33 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
   hipLaunchKernelGGL(x3_wgrad_kernel, grid, dim3(kTrainThreads), 0, as_stream(stream), A, lda, M,
                      B, ldb, N, P, chunk, amax_a, amax_b, part, bias_part);
   return check_launch("x3_wgrad_kernel");
+}
+
+
+extern "C" int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks,
+                                   nerf_stream_t stream) {
+  NERF_REQUIRE(descs && n >= 1 && n <= kWgBatchMax && chunks >= 1 && chunks < 65536,
+               "nerf_x3_wgrad_batch: bad arguments");
+  WgradBatch bt;
+  int64_t tiles = 0;
+  for (int k = 0; k < n; ++k) {
+    const NerfWgradDesc& d = descs[k];
+    NERF_REQUIRE(d.A && d.B && d.amax_a && d.amax_b && d.part && d.M > 0 && d.N > 0 &&
+                     d.P >= 0 && d.lda >= d.P && d.ldb >= d.P && d.ldpart >= (int64_t)d.M * d.N &&
+                     (!d.bias_part || d.ldbias >= d.M),
+                 "nerf_x3_wgrad_batch: bad descriptor");
+    NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P),
+                 "nerf_x3_wgrad_batch: operands must be aligned (P % 32 == 0, 16-B rows, < 2 GiB)");
+    bt.d[k] = d;
+    tiles += (int64_t)cdiv(d.M, kWgTile) * cdiv(d.N, kWgTile);
+    bt.tiles_end[k] = (int)tiles;
+  }
+  bt.n = n;
+  bt.Z = chunks;
+  NERF_REQUIRE(tiles * chunks < (1ll << 31), "nerf_x3_wgrad_batch: too many workgroups");
+  hipLaunchKernelGGL(x3_wgrad_batch_kernel, dim3((unsigned)(tiles * chunks)), dim3(kTrainThreads),
+                     0, as_stream(stream), bt);
+  return check_launch("x3_wgrad_batch_kernel");
 }
 
 extern "C" int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream) {

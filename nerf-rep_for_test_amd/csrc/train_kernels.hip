@@ -408,6 +408,38 @@ int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
   return check_launch("sample_pdf_bwd_kernel");
 }
 
+// out[i] = sum over c = 0..C-1 (in that order) of part[c * n + i]: the split-K
+// partials of the weight-gradient kernel summed in a fixed order. One output
+// per lane, 8 partials in flight per lane (the partials are re-read right
+// after they were written, mostly from the Infinity Cache).
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ part,
+                                                           int64_t C, int64_t n,
+                                                           float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float* p = part + i;
+  float s = 0.0f;
+  int64_t c = 0;
+  for (; c + 8 <= C; c += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[(c + k) * n];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  for (; c < C; ++c) s += p[c * n];
+  out[i] = s;
+}
+
+int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream) {
+  NERF_REQUIRE(part && out, "nerf_sum_partials: null pointer");
+  NERF_REQUIRE(C >= 1 && n >= 0, "nerf_sum_partials: bad size");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), part, C, n, out);
+  return check_launch("sum_partials_kernel");
+}
+
 }  // extern "C"
 
 }  // namespace nerfhip

@@ -24,6 +24,8 @@ ops, no host sync): packing order = ``pack_x3_matrix``.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -149,11 +151,24 @@ def _packs_for(params, device):
 
 
 def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, rw=None,
-           amax=None):
-    """One nerf_x3_layer launch; amax (a device float, >= 0) is raised to max |C|."""
-    call("nerf_x3_layer", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0), ptr(mask),
-         mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu), ptr(C),
-         C.stride(0), P, ptr(amax), _lib.stream_of(C.device))
+           amax=None, bits_out=None, mask_bits=None):
+    """One nerf_x3_layer launch; amax (a device float, >= 0) is raised to max |C|.
+    bits_out (int16 words, relu only) receives the ReLU mask of C as bits;
+    mask_bits (such words, instead of mask) masks C (nerf_x3_layer_bits)."""
+    if bits_out is None and mask_bits is None:
+        call("nerf_x3_layer", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0),
+             ptr(mask), mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu),
+             ptr(C), C.stride(0), P, ptr(amax), _lib.stream_of(C.device))
+        return
+    call("nerf_x3_layer_bits", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0),
+         ptr(mask), mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu),
+         ptr(C), C.stride(0), P, ptr(amax), ptr(bits_out), ptr(mask_bits),
+         _lib.stream_of(C.device))
+
+
+def relu_bits_words(P, m_tiles):
+    """int16 words of one layer's ReLU mask (nerf_x3_layer_bits layout)."""
+    return -(-P // 128) * 128 * m_tiles
 
 
 def _encode(x, n_freq, out, amax):
@@ -179,10 +194,95 @@ def _wgrad(A, B, amax_a=None, amax_b=None, with_bias=False):
     bpart = torch.empty((chunks, M), device=A.device, dtype=torch.float32) if with_bias else None
     amax_a = _absmax(A) if amax_a is None else amax_a
     amax_b = _absmax(B) if amax_b is None else amax_b
+    st = _lib.stream_of(A.device)
     call("nerf_x3_wgrad", ptr(A), A.stride(0), M, ptr(B), B.stride(0), N, P, chunk,
-         ptr(amax_a), ptr(amax_b), ptr(part), ptr(bpart), _lib.stream_of(A.device))
-    dw = part.sum(0)
-    return (dw, bpart.sum(0)) if with_bias else dw
+         ptr(amax_a), ptr(amax_b), ptr(part), ptr(bpart), st)
+    dw = torch.empty((M, N), device=A.device, dtype=torch.float32)
+    call("nerf_sum_partials", ptr(part), chunks, M * N, ptr(dw), st)
+    if not with_bias:
+        return dw
+    db = torch.empty((M,), device=A.device, dtype=torch.float32)
+    call("nerf_sum_partials", ptr(bpart), chunks, M, ptr(db), st)
+    return dw, db
+
+
+class _WgradDesc(ctypes.Structure):
+    """NerfWgradDesc (include/nerfhip.h)."""
+    _fields_ = [("A", ctypes.c_void_p), ("lda", ctypes.c_int64), ("B", ctypes.c_void_p),
+                ("ldb", ctypes.c_int64), ("P", ctypes.c_int64), ("amax_a", ctypes.c_void_p),
+                ("amax_b", ctypes.c_void_p), ("part", ctypes.c_void_p),
+                ("ldpart", ctypes.c_int64), ("bias_part", ctypes.c_void_p),
+                ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int)]
+
+
+def _dma_ok(t):
+    return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
+class WgradBatch:
+    """The weight gradients of one backward, deferred and computed together by
+    ONE nerf_x3_wgrad_batch launch (each split over ~256 / tiles sample subsets,
+    so the split-K partials are ~10x fewer than per-layer launches), then ONE
+    fixed-order partial sum for all weights and one for all biases.
+    add() returns a slot; results()[slot] = (dW[, db]). Requests whose operands
+    the batched kernel cannot take (P % 32, alignment) run through _wgrad."""
+
+    def __init__(self, device):
+        self.device = device
+        self.req = []
+
+    def add(self, A, B, amax_a=None, amax_b=None, with_bias=False):
+        if amax_a is None:
+            amax_a = _absmax(A)
+        if amax_b is None:
+            amax_b = _absmax(B)
+        self.req.append((A, B, amax_a, amax_b, with_bias))
+        return len(self.req) - 1
+
+    def results(self):
+        req, self.req = self.req, []
+        if not req:
+            return []
+        P = req[0][0].shape[1]
+        ok = (len(req) <= 16 and P % 32 == 0 and
+              all(A.shape[1] == P and B.shape[1] == P and _dma_ok(A) and _dma_ok(B)
+                  and A.numel() * 4 < (1 << 31) and B.numel() * 4 < (1 << 31)
+                  for A, B, *_ in req))
+        if not ok:
+            return [_wgrad(A, B, aa, ab, wb) for A, B, aa, ab, wb in req]
+        tiles = sum(-(-A.shape[0] // 256) * -(-B.shape[0] // 256) for A, B, *_ in req)
+        Z = max(1, min(P // 32, 256 // tiles))
+        sizes = [A.shape[0] * B.shape[0] for A, B, *_ in req]
+        bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb in req]
+        ld, ldb = sum(sizes), max(1, sum(bsizes))
+        part = torch.empty((Z, ld), device=self.device, dtype=torch.float32)
+        bpart = torch.empty((Z, ldb), device=self.device, dtype=torch.float32)
+        descs = (_WgradDesc * len(req))()
+        off = boff = 0
+        for k, (A, B, aa, ab, wb) in enumerate(req):
+            descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
+                                  aa.data_ptr(), ab.data_ptr(), part.data_ptr() + 4 * off, ld,
+                                  bpart.data_ptr() + 4 * boff if wb else None, ldb,
+                                  A.shape[0], B.shape[0])
+            off += sizes[k]
+            boff += bsizes[k]
+        st = _lib.stream_of(self.device)
+        call("nerf_x3_wgrad_batch", ctypes.addressof(descs), len(req), Z, st)
+        flat = torch.empty((ld,), device=self.device, dtype=torch.float32)
+        call("nerf_sum_partials", ptr(part), Z, ld, ptr(flat), st)
+        bflat = torch.empty((ldb,), device=self.device, dtype=torch.float32)
+        if boff:
+            call("nerf_sum_partials", ptr(bpart), Z, ldb, ptr(bflat), st)
+        out, off, boff = [], 0, 0
+        for k, (A, B, _, _, wb) in enumerate(req):
+            dw = flat[off:off + sizes[k]].view(A.shape[0], B.shape[0])
+            off += sizes[k]
+            if wb:
+                out.append((dw, bflat[boff:boff + bsizes[k]]))
+                boff += bsizes[k]
+            else:
+                out.append(dw)
+        return out
 
 
 PARAM_NAMES = ([f"pts_linears.{i}.{k}" for i in range(8) for k in ("weight", "bias")] +
@@ -235,11 +335,14 @@ class NerfMLPFn(torch.autograd.Function):
         H[4] = E[64:320]
         pk = _packs_for(params, dev)
         src = E[0:64]
+        # the ReLU masks of h0..h7 as bits for the dgrad launches (32 B per sample
+        # and layer instead of re-reading the 1 KiB of FP32 activations)
+        bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
         for i in range(8):
             wp, sw, mt, nk = pk[f"fwd{i}"]
             B = E if i == 5 else src
             _layer(wp, sw, mt, nk, B, H[i], P, bias=p[f"pts_linears.{i}.bias"], relu=True,
-                   amax=amax[i:i + 1])
+                   amax=amax[i:i + 1], bits_out=bits[i])
             src = H[i]
         h7 = H[7]
         alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
@@ -255,14 +358,14 @@ class NerfMLPFn(torch.autograd.Function):
                amax=amax[11:12])
         rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
         raw = torch.cat([rgb, alpha], 0).t().contiguous()
-        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, *params)
+        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, *params)
         ctx.pts_grad = pts.requires_grad
         ctx.packs = pk
         return raw
 
     @staticmethod
     def backward(ctx, d_raw):
-        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, *params = ctx.saved_tensors
+        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, *params = ctx.saved_tensors
         H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
         p = dict(zip(PARAM_NAMES, params))
         pk = ctx.packs
@@ -272,40 +375,38 @@ class NerfMLPFn(torch.autograd.Function):
         grads = {}
         d_raw = d_raw.t().contiguous()                              # [4, P]
         d_rgb, d_sig = d_raw[0:3], d_raw[3:4]
-        grads["rgb_linear.weight"] = _wgrad(d_rgb, HV, amax_b=amax[11:12])   # K = P: x3 split-K
+        wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
+        post = {}              # slot -> (weight name, bias name or None, column fix-up)
+        post[wb.add(d_rgb, HV, amax_b=amax[11:12])] = ("rgb_linear.weight", None, None)
         grads["rgb_linear.bias"] = d_rgb.sum(1)
         d_hv = (p["rgb_linear.weight"].t() @ d_rgb) * (HV > 0)      # [128, P]
         wv = p["views_linears.0.weight"]                            # [128, 283]
-        gw, gb = _wgrad(d_hv, V, amax_b=torch.maximum(amax[8:9], amax[10:11]), with_bias=True)
-        grads["views_linears.0.weight"] = gw[:, :283]
-        grads["views_linears.0.bias"] = gb
+        post[wb.add(d_hv, V, amax_b=torch.maximum(amax[8:9], amax[10:11]), with_bias=True)] = (
+            "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
         dmax = torch.zeros(10, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
         wvt, swvt, mt, nk = pk["bwd_views"]
         DF = _act(256, P, dev)
         _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
-        grads["feature_linear.weight"], grads["feature_linear.bias"] = _wgrad(
-            DF, H[7], dmax[8:9], amax[7:8], with_bias=True)
-        grads["alpha_linear.weight"] = _wgrad(d_sig, H[7], amax_b=amax[7:8])
+        post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
+            "feature_linear.weight", "feature_linear.bias", None)
+        post[wb.add(d_sig, H[7], amax_b=amax[7:8])] = ("alpha_linear.weight", None, None)
         grads["alpha_linear.bias"] = d_sig.sum(1)
         # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
         wft, swft, _, _ = pk["bwd_feat"]
         D = _act(256, P, dev)
         aw = p["alpha_linear.weight"].reshape(-1).contiguous()
         dsig = d_sig.reshape(-1).contiguous()
-        _layer(wft, swft, 16, 8, DF, D, P, mask=H[7], ru=aw, rw=dsig, amax=dmax[7:8])
+        _layer(wft, swft, 16, 8, DF, D, P, mask_bits=bits[7], ru=aw, rw=dsig, amax=dmax[7:8])
         d_enc = None
         for i in range(7, -1, -1):
             inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
             in_max = (torch.maximum(amax[9:10], amax[4:5]) if i == 5 else
                       amax[9:10] if i == 0 else amax[i - 1:i])
-            gw, gb = _wgrad(D, inp, dmax[i:i + 1], in_max, with_bias=True)
-            if i == 0:
-                gw = gw[:, :63]
-            elif i == 5:
-                gw = torch.cat([gw[:, :63], gw[:, 64:320]], 1)
-            grads[f"pts_linears.{i}.weight"] = gw
-            grads[f"pts_linears.{i}.bias"] = gb
+            fix = ((lambda g: g[:, :63]) if i == 0 else
+                   (lambda g: torch.cat([g[:, :63], g[:, 64:320]], 1)) if i == 5 else None)
+            post[wb.add(D, inp, dmax[i:i + 1], in_max, with_bias=True)] = (
+                f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", fix)
             need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
             if i == 0:
                 if need_enc:
@@ -317,7 +418,7 @@ class NerfMLPFn(torch.autograd.Function):
             Dn = _act(256, P, dev)
             if i == 5:
                 wt, swt, mt, nk = pk["bwd5h"]
-                _layer(wt, swt, mt, nk, D, Dn, P, mask=H[4], amax=dmax[i - 1:i])
+                _layer(wt, swt, mt, nk, D, Dn, P, mask_bits=bits[4], amax=dmax[i - 1:i])
                 if need_enc:
                     we, swe, mt, nk = pk["bwd5e"]
                     de = _act(64, P, dev)
@@ -325,8 +426,14 @@ class NerfMLPFn(torch.autograd.Function):
                     d_enc = de[:63]
             else:
                 wt, swt, mt, nk = pk[f"bwd{i}"]
-                _layer(wt, swt, mt, nk, D, Dn, P, mask=H[i - 1], amax=dmax[i - 1:i])
+                _layer(wt, swt, mt, nk, D, Dn, P, mask_bits=bits[i - 1], amax=dmax[i - 1:i])
             D = Dn
+        for slot, res in enumerate(wb.results()):
+            wname, bname, fix = post[slot]
+            gw, gb = (res if bname else (res, None))
+            grads[wname] = fix(gw) if fix is not None else gw
+            if bname:
+                grads[bname] = gb
         d_pts = None
         if d_enc is not None:
             d_pts = torch.empty((P, 3), device=dev, dtype=f32)

@@ -225,3 +225,45 @@ def test_x3_train_mlp_denormal_sample_gradients(dev):
     for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads):
         assert torch.isfinite(a).all(), name
         assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("nk", [2, 8, 10])
+def test_x3_layer_relu_bits_roundtrip(dev, nk):
+    """A forward launch writes its ReLU mask as bits (nerf_x3_layer_bits); a
+    masked dgrad launch reading those bits is bitwise equal to the same launch
+    masked by the FP32 activations, for ragged P (invalid samples' bits 0)."""
+    from nerfhip.train_mlp import _layer, pack_x3_matrix, relu_bits_words
+    g = torch.Generator(device=dev).manual_seed(11)
+    for P in (1, 300, 1000):
+        K = 32 * nk
+        W = torch.randn((256, K), device=dev, generator=g) * 0.1
+        B = torch.randn((K, P), device=dev, generator=g)
+        bias = torch.randn(256, device=dev, generator=g) * 0.05
+        wp, sw = pack_x3_matrix(W)
+        H = torch.empty((256, P), device=dev)
+        H2 = torch.empty((256, P), device=dev)
+        bits = torch.full((relu_bits_words(P, 16),), -1, device=dev, dtype=torch.int16)
+        _layer(wp, sw, 16, nk, B, H, P, bias=bias, relu=True, bits_out=bits)
+        _layer(wp, sw, 16, nk, B, H2, P, bias=bias, relu=True)
+        assert torch.equal(H, H2)              # the bits do not change the forward
+        # decode: u16 word ((p // 128 * 8 + p % 128 // 16) * 4 + m // 64) * 64
+        # + p % 16 + 16 (m % 16 // 4), bit 4 (m % 64 // 16) + m % 4
+        p = torch.arange(P, device=dev)[None, :]
+        m = torch.arange(256, device=dev)[:, None]
+        word = ((p // 128 * 8 + p % 128 // 16) * 4 + m // 64) * 64 + p % 16 + 16 * (m % 16 // 4)
+        bit = 4 * (m % 64 // 16) + m % 4
+        got = (bits.to(torch.int32)[word] >> bit) & 1
+        assert torch.equal(got.bool(), H > 0)
+        Wb = torch.randn((256, 256), device=dev, generator=g) * 0.1
+        wpb, swb = pack_x3_matrix(Wb)
+        D = torch.randn((256, P), device=dev, generator=g)
+        Cf = torch.empty((256, P), device=dev)
+        Cb = torch.empty((256, P), device=dev)
+        _layer(wpb, swb, 16, 8, D, Cf, P, mask=H)
+        _layer(wpb, swb, 16, 8, D, Cb, P, mask_bits=bits)
+        assert torch.equal(Cf, Cb)
+        ru = torch.randn(256, device=dev, generator=g)
+        rw = torch.randn(P, device=dev, generator=g)
+        _layer(wpb, swb, 16, 8, D, Cf, P, mask=H, ru=ru, rw=rw)
+        _layer(wpb, swb, 16, 8, D, Cb, P, mask_bits=bits, ru=ru, rw=rw)
+        assert torch.equal(Cf, Cb)
