@@ -495,3 +495,32 @@ def test_ert_compaction_frame_with_grid_update(dev):
     for k in outs[0][0]:
         assert torch.equal(outs[0][0][k], outs[1][0][k]), k
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("S,NI,kind", [(64, 128, "lin"), (32, 64, "lin"), (48, 16, "lin"),
+                                       (64, 128, "zeros"), (5, 7, "lin"), (64, 128, "perm"),
+                                       (130, 256, "lin")])
+def test_sample_fine_shared_u(dev, S, NI, kind):
+    """One shared u row (u_stride 0, as eval passes linspace): the merge-path
+    fast path (ascending u, n_imp and S + n_imp multiples of 16), its fallbacks
+    (a shared row that is not ascending; weights with zero bins, where the
+    denom clamp can make the inverse CDF non-monotonic and the row is sorted
+    first) and ragged sizes that never take it; bit-exact vs the oracle."""
+    rng = np.random.default_rng(11 + S + NI)
+    n = 257
+    zc = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    wc = (rng.random((n, S)) ** 4).astype(np.float32)
+    if kind == "zeros":
+        wc[rng.random((n, S)) < 0.7] = 0.0
+    u = O.linspace_f32(0, 1, NI)
+    if kind == "perm":
+        u = u[rng.permutation(NI)]
+    zall = torch.empty((n, S + NI), device=dev)
+    from nerfhip._lib import call, ptr, stream_of
+    zc_d, wc_d, u_d = _t(zc, dev), _t(wc, dev), _t(np.ascontiguousarray(u), dev)
+    call("nerf_sample_fine", ptr(zc_d), S, ptr(wc_d), ptr(u_d), 0, n, S, NI, ptr(zall),
+         stream_of(dev))
+    mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
+    ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1],
+                                                   np.broadcast_to(u, (n, NI)))], -1), -1)
+    assert np.array_equal(zall.cpu().numpy(), ref)
