@@ -496,39 +496,15 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
     if (k < pc && s < nw) cdf[s + 1] = (float)run;
   }
   __builtin_amdgcn_wave_barrier();
-  // inverse CDF (searchsorted right=True, clamp, lerp; VR:254-266).
-  // contig (eval: one shared, ascending u row, e.g. linspace): lane t takes the
-  // fine samples j = t * qpl + q, so its queries ascend and one binary search
-  // plus a forward walk places them all; the merge with the coarse row below is
-  // then a merge path with contiguous output runs. Otherwise j = t + 16 q.
+  // inverse CDF (searchsorted right=True, clamp, lerp; VR:254-266); fine sample
+  // j = t + 16 q of this lane
   const float* ur = u + (live ? ray : 0) * u_stride;
-  const int qpl = n_imp / FINE_LANES;
-  bool contig = u_stride == 0 && n_imp % FINE_LANES == 0 && (S + n_imp) % FINE_LANES == 0;
-  if (contig) {   // the shared row ascends (uniform over the wave: every ray reads it)
-    bool desc = false;
-    for (int j = lane; j + 1 < n_imp; j += 64) desc |= u[j] > u[j + 1];
-    contig = __ballot(desc) == 0ull;
-  }
-  const int nq = contig ? qpl : (t < n_imp ? (n_imp - 1 - t) / FINE_LANES + 1 : 0);
-  const int jbase = contig ? t * qpl : t, jstep = contig ? 1 : FINE_LANES;
+  const int nq = t < n_imp ? (n_imp - 1 - t) / FINE_LANES + 1 : 0;
   float x[QN];
   int pos[QN];
 #pragma unroll
-  for (int q = 0; q < QN; ++q) x[q] = q < nq ? ur[jbase + jstep * q] : 0.0f;
-  if (contig) {
-    float x0[1] = {x[0]};
-    int p0[1];
-    fine_search<true>(cdf, nb, x0, p0);
-    int pp = p0[0];
-#pragma unroll
-    for (int q = 0; q < QN; ++q) {
-      if (q > 0 && q < nq)
-        while (pp < nb && cdf[pp] <= x[q]) ++pp;
-      pos[q] = pp;
-    }
-  } else {
-    fine_search<true>(cdf, nb, x, pos);
-  }
+  for (int q = 0; q < QN; ++q) x[q] = q < nq ? ur[t + FINE_LANES * q] : 0.0f;
+  fine_search<true>(cdf, nb, x, pos);
 #pragma unroll
   for (int q = 0; q < QN; ++q) {   // (queries q >= nq run on u = 0 and are never stored)
     const int inds = pos[q];
@@ -545,7 +521,7 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
   __builtin_amdgcn_wave_barrier();   // every read of the staged weights is done
 #pragma unroll
   for (int q = 0; q < QN; ++q)
-    if (q < nq) zf[jbase + jstep * q] = x[q];
+    if (q < nq) zf[t + FINE_LANES * q] = x[q];
   for (int j = n_imp + t; j < p2; j += FINE_LANES) zf[j] = __builtin_inff();
   __builtin_amdgcn_wave_barrier();
   // ascending bitonic sort of the (inf-padded) fine samples, per ray, skipped
@@ -554,49 +530,7 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
   bool unsorted = false;
   for (int j = t; j + 1 < n_imp; j += FINE_LANES) unsorted |= zf[j] > zf[j + 1];
   const unsigned long long bal = __ballot(unsorted);
-  const bool ray_unsorted = (bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull;
-  if (contig && !ray_unsorted) {
-    // merge path: lane t writes merged outputs [D0, D0 + per) of the row; the
-    // coarse elements among the first D0 = the first i with zc[i] > zf[D0-i-1]
-    // (ties: coarse first, as the rank merge below; equal values are
-    // interchangeable)
-    if (!live) return;
-    const int per = (S + n_imp) / FINE_LANES, D0 = t * per;
-    int lo = D0 - n_imp > 0 ? D0 - n_imp : 0, hi = D0 < S ? D0 : S;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (zc[mid] <= zf[D0 - mid - 1]) lo = mid + 1;
-      else hi = mid;
-    }
-    int i = lo, j = D0 - lo;
-    float* out = z_all + ray * (int64_t)(S + n_imp) + D0;
-    if ((per & 3) == 0) {
-      for (int k = 0; k < per; k += 4) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool takec = i < S && (j >= n_imp || zc[i] <= zf[j]);
-          v[e] = takec ? zc[i] : zf[j];
-          i += takec;
-          j += !takec;
-        }
-        *reinterpret_cast<float4*>(out + k) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    } else {
-      for (int k = 0; k < per; ++k) {
-        const bool takec = i < S && (j >= n_imp || zc[i] <= zf[j]);
-        out[k] = takec ? zc[i] : zf[j];
-        i += takec;
-        j += !takec;
-      }
-    }
-    return;
-  }
-  if (contig) {   // back to the strided layout the sort and the rank merge use
-#pragma unroll
-    for (int q = 0; q < QN; ++q) x[q] = zf[t + FINE_LANES * q];
-  }
-  if (ray_unsorted) {
+  if ((bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull) {
     for (int k = 2; k <= p2; k <<= 1) {
       for (int jj = k >> 1; jj > 0; jj >>= 1) {
         for (int i = t; i < p2; i += FINE_LANES) {
