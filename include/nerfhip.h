@@ -155,19 +155,25 @@ int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_tiles, int k_
                   const float* bias, const float* B, int64_t ldb, const float* mask,
                   int64_t ldm, const float* ru, const float* rw, int relu, float* C,
                   int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream);
-/* nerf_x3_layer_bits: nerf_x3_layer with the ReLU mask carried as bits.
+/* nerf_x3_layer_ex: nerf_x3_layer with the ReLU mask carried as bits and an
+ *   optional output head.
  *   relu_bits (nullable, needs relu) receives bit (C[m][p] > 0) of every output
  *   element; mask_bits (nullable, instead of mask) multiplies C by such a bit.
  *   Layout: u16 word ((p / 128 * 8 + p % 128 / 16) * m_tiles / 4 + m / 64) * 64
  *   + (p % 16) + 16 * (m % 16 / 4), bit 4 * (m % 64 / 16) + m % 4: the layer
- *   kernel's own lane order, so producer and consumer have the same m_tiles
- *   (16: the 256-wide layers); ceil(P / 128) * 128 * m_tiles words. 32 B per
- *   sample and 256-wide layer, where the FP32 mask is 1 KiB. */
-int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
-                       const float* bias, const float* B, int64_t ldb, const float* mask,
-                       int64_t ldm, const float* ru, const float* rw, int relu, float* C,
-                       int64_t ldc, int64_t P, float* amax_out, unsigned short* relu_bits,
-                       const unsigned short* mask_bits, nerf_stream_t stream);
+ *   kernel's own lane order, so producer and consumer have the same m_tiles;
+ *   ceil(P / 128) * 128 * m_tiles words. 32 B per sample and 256-wide layer,
+ *   where the FP32 mask is 1 KiB.
+ *   head_out (nullable): head_out[p * 4 + head_col + c] = sum_m head_w[c * 16 *
+ *   m_tiles + m] * C[m][p] + head_b[c] for c < n_head (1..3, head_col + n_head
+ *   <= 4; head_w 16-byte aligned): the alpha / rgb heads (network.py:61, 68-70)
+ *   written straight into raw [P][4]. */
+int nerf_x3_layer_ex(const float* w_packed, const int* w_scale, int m_tiles, int k_steps,
+                     const float* bias, const float* B, int64_t ldb, const float* mask,
+                     int64_t ldm, const float* ru, const float* rw, int relu, float* C,
+                     int64_t ldc, int64_t P, float* amax_out, unsigned short* relu_bits,
+                     const unsigned short* mask_bits, const float* head_w, const float* head_b,
+                     int n_head, float* head_out, int head_col, nerf_stream_t stream);
 int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                   int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
                   float* part, float* bias_part, nerf_stream_t stream);

@@ -636,8 +636,12 @@ __device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op
 // wave * 16 + (lane & 15)) and rows 16 (u0 + t) + 4 (lane >> 4) + r, bit
 // 4 t + r, as one u16 at ((tile * 8 + wave) * MT / 4 + u0 / 4) * 64 + lane:
 // 32 B per sample and 256-row layer instead of the 1 KiB of the FP32 mask.
+// kEpiHead: a head of n_head (1..3) outputs on the final C of the sample,
+// head_out[p * 4 + head_col + c] = sum_m head_w[c][m] C[m][p] + head_b[c] (the
+// alpha head on h7 and the rgb head on the views output, NET:61, 68-70,
+// written straight into raw [P][4]): no second pass over C.
 enum : int { kEpiBias = 1, kEpiRelu = 2, kEpiMask = 4, kEpiRank1 = 8, kEpiMaskBits = 16,
-             kEpiOutBits = 32 };
+             kEpiOutBits = 32, kEpiHead = 64 };
 
 __device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n uniform
   switch (n) {
@@ -662,7 +666,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
     const float* __restrict__ mask, int64_t ldm, const float* __restrict__ ru,
     const float* __restrict__ rw, float* __restrict__ C, int64_t ldc, int64_t P,
     float* __restrict__ amax_out, unsigned short* __restrict__ bits_out,
-    const unsigned short* __restrict__ bits_in) {
+    const unsigned short* __restrict__ bits_in, const float* __restrict__ head_w,
+    const float* __restrict__ head_b, int n_head, float* __restrict__ head_out, int head_col) {
   constexpr int kPieces = 2 * MT;          // 1-KiB LDS-DMA pieces per slice
   constexpr int kSliceU4 = kPieces * 64;
   constexpr int kPpw = kPieces / 8;        // pieces per wave
@@ -783,6 +788,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
       voc[r] = valid ? (unsigned)(((int64_t)(4 * g4 + r) * ldc + p) * 4) : (unsigned)nbC;
       vom[r] = valid ? (unsigned)(((int64_t)(4 * g4 + r) * ldm + p) * 4) : (unsigned)nbM;
     }
+    float hpart[3] = {0.0f, 0.0f, 0.0f};   // kEpiHead: this lane's share of each output
     // epilogue in blocks of 4 tiles: every load of a block issued before its use
 #pragma unroll
     for (int u0 = 0; u0 < MT; u0 += 4) {
@@ -830,6 +836,31 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
                                                 (int)voc[r], (int)(16u * (u0 + t) * ldc4), 0);
           omax = valid ? fmaxf(omax, fabsf(v[t][r])) : omax;
         }
+      if constexpr ((EPI & kEpiHead) != 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (c < n_head) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const float4 hw = *reinterpret_cast<const float4*>(
+                  head_w + c * 16 * MT + 16 * (u0 + t) + 4 * g4);
+              hpart[c] = __builtin_fmaf(v[t][0], hw.x, hpart[c]);
+              hpart[c] = __builtin_fmaf(v[t][1], hw.y, hpart[c]);
+              hpart[c] = __builtin_fmaf(v[t][2], hw.z, hpart[c]);
+              hpart[c] = __builtin_fmaf(v[t][3], hw.w, hpart[c]);
+            }
+          }
+        }
+      }
+    }
+    if constexpr ((EPI & kEpiHead) != 0) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (c < n_head) {
+          const float h = quad_sum(hpart[c]) + head_b[c];
+          if (valid && g4 == 0) head_out[p * 4 + head_col + c] = h;
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile starts clean
   }
@@ -1312,13 +1343,15 @@ static int launch_layer(const float* w, const int* sw, const float* bias, const 
                         int64_t ldb, const float* mask, int64_t ldm, const float* ru,
                         const float* rw, float* C, int64_t ldc, int64_t P, float* amax_out,
                         unsigned short* bits_out, const unsigned short* bits_in,
-                        nerf_stream_t stream) {
+                        const float* head_w, const float* head_b, int n_head, float* head_out,
+                        int head_col, nerf_stream_t stream) {
   // persistent: at most one workgroup per CU (the ring takes 64-128 KiB of LDS)
   const int64_t tiles = cdiv(P, kTrainTile);
   const int n_cu = stream_cu_count(stream);
   hipLaunchKernelGGL((x3_layer_kernel<MT, NK, EPI>), dim3((unsigned)(tiles < n_cu ? tiles : n_cu)),
                      dim3(kTrainThreads), 0, as_stream(stream), (const uint4*)w, sw, bias, B,
-                     ldb, mask, ldm, ru, rw, C, ldc, P, amax_out, bits_out, bits_in);
+                     ldb, mask, ldm, ru, rw, C, ldc, P, amax_out, bits_out, bits_in, head_w,
+                     head_b, n_head, head_out, head_col);
   return check_launch("x3_layer_kernel");
 }
 
@@ -1326,16 +1359,22 @@ extern "C" int nerf_x3_layer(const float* w_packed, const int* w_scale, int m_ti
                              const float* bias, const float* B, int64_t ldb, const float* mask,
                              int64_t ldm, const float* ru, const float* rw, int relu, float* C,
                              int64_t ldc, int64_t P, float* amax_out, nerf_stream_t stream) {
-  return nerf_x3_layer_bits(w_packed, w_scale, m_tiles, k_steps, bias, B, ldb, mask, ldm, ru, rw,
-                            relu, C, ldc, P, amax_out, nullptr, nullptr, stream);
+  return nerf_x3_layer_ex(w_packed, w_scale, m_tiles, k_steps, bias, B, ldb, mask, ldm, ru, rw,
+                          relu, C, ldc, P, amax_out, nullptr, nullptr, nullptr, nullptr, 0,
+                          nullptr, 0, stream);
 }
 
-extern "C" int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int m_tiles,
-                                  int k_steps, const float* bias, const float* B, int64_t ldb,
-                                  const float* mask, int64_t ldm, const float* ru, const float* rw,
-                                  int relu, float* C, int64_t ldc, int64_t P, float* amax_out,
-                                  unsigned short* relu_bits, const unsigned short* mask_bits,
-                                  nerf_stream_t stream) {
+extern "C" int nerf_x3_layer_ex(const float* w_packed, const int* w_scale, int m_tiles,
+                                int k_steps, const float* bias, const float* B, int64_t ldb,
+                                const float* mask, int64_t ldm, const float* ru, const float* rw,
+                                int relu, float* C, int64_t ldc, int64_t P, float* amax_out,
+                                unsigned short* relu_bits, const unsigned short* mask_bits,
+                                const float* head_w, const float* head_b, int n_head,
+                                float* head_out, int head_col, nerf_stream_t stream) {
+  NERF_REQUIRE(!head_out || (head_w && head_b && n_head >= 1 && n_head <= 3 && head_col >= 0 &&
+                             head_col + n_head <= 4 && ((uintptr_t)head_w & 15) == 0),
+               "nerf_x3_layer: head needs 16-byte aligned head_w [n_head][16 m_tiles], head_b, "
+               "1 <= n_head <= 3 columns inside [0, 4)");
   NERF_REQUIRE(w_packed && w_scale && B && C, "nerf_x3_layer: null pointer");
   NERF_REQUIRE(!(mask && mask_bits), "nerf_x3_layer: mask and mask_bits are exclusive");
   NERF_REQUIRE(!relu_bits || relu, "nerf_x3_layer: relu_bits needs relu");
@@ -1351,11 +1390,12 @@ extern "C" int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int
   if (P == 0) return 0;
   const int epi = (bias ? kEpiBias : 0) | (relu ? kEpiRelu : 0) | (mask ? kEpiMask : 0) |
                   (ru ? kEpiRank1 : 0) | (mask_bits ? kEpiMaskBits : 0) |
-                  (relu_bits ? kEpiOutBits : 0);
+                  (relu_bits ? kEpiOutBits : 0) | (head_out ? kEpiHead : 0);
 #define NERF_LAYER_CASE(MT, NK, EPI)                                                          \
   if (m_tiles == MT && k_steps == NK && epi == (EPI))                                         \
     return launch_layer<MT, NK, (EPI)>(w_packed, w_scale, bias, B, ldb, mask, ldm, ru, rw, C, \
-                                       ldc, P, amax_out, relu_bits, mask_bits, stream);
+                                       ldc, P, amax_out, relu_bits, mask_bits, head_w, head_b,   \
+                                       n_head, head_out, head_col, stream);
   // forward layers (bias + ReLU; the feature layer without ReLU)
   NERF_LAYER_CASE(16, 2, kEpiBias | kEpiRelu) NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu)
   NERF_LAYER_CASE(16, 10, kEpiBias | kEpiRelu) NERF_LAYER_CASE(8, 9, kEpiBias | kEpiRelu)
@@ -1369,6 +1409,11 @@ extern "C" int nerf_x3_layer_bits(const float* w_packed, const int* w_scale, int
   NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiOutBits)
   NERF_LAYER_CASE(16, 10, kEpiBias | kEpiRelu | kEpiOutBits)
   NERF_LAYER_CASE(16, 8, kEpiMaskBits) NERF_LAYER_CASE(16, 8, kEpiMaskBits | kEpiRank1)
+  // + the heads: alpha on layer 7, rgb on the views layer (which also writes its
+  // bits for the d_hv launch (8, 1, mask bits))
+  NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiOutBits | kEpiHead)
+  NERF_LAYER_CASE(8, 9, kEpiBias | kEpiRelu | kEpiOutBits | kEpiHead)
+  NERF_LAYER_CASE(8, 1, kEpiMaskBits)
   // every term at once (tests)
   NERF_LAYER_CASE(16, 8, kEpiBias | kEpiRelu | kEpiMask | kEpiRank1)
 #undef NERF_LAYER_CASE

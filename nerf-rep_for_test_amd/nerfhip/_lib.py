@@ -30,8 +30,8 @@ SIGNATURES = {
     "nerf_ert_segment": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _I, _I, _F, _P, _P, _P, _P, _S]),
     "nerf_x3_layer": (_I, [_P, _P, _I, _I, _P, _P, _I64, _P, _I64, _P, _P, _I, _P, _I64, _I64,
                            _P, _S]),
-    "nerf_x3_layer_bits": (_I, [_P, _P, _I, _I, _P, _P, _I64, _P, _I64, _P, _P, _I, _P, _I64,
-                                _I64, _P, _P, _P, _S]),
+    "nerf_x3_layer_ex": (_I, [_P, _P, _I, _I, _P, _P, _I64, _P, _I64, _P, _P, _I, _P, _I64,
+                              _I64, _P, _P, _P, _P, _P, _I, _P, _I, _S]),
     "nerf_sum_partials": (_I, [_P, _I64, _I64, _P, _S]),
     "nerf_x3_wgrad_batch": (_I, [_P, _I, _I, _S]),
     "nerf_x3_wgrad": (_I, [_P, _I64, _I, _P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _S]),

@@ -94,7 +94,9 @@ class X3Packer:
                 "bwd_feat": ("feature_linear.weight", True, ar(256), ar(256)),
                 "bwd5h": ("pts_linears.5.weight", True, list(range(63, 319)), ar(256)),
                 "bwd5e": ("pts_linears.5.weight", True, enc64, ar(256)),
-                "bwd0": ("pts_linears.0.weight", True, enc64, ar(256))}
+                "bwd0": ("pts_linears.0.weight", True, enc64, ar(256)),
+                # d hv = W_rgb^T d_rgb: K = the 3 rgb rows of d_raw^T (+ 29 zero rows)
+                "bwd_rgb": ("rgb_linear.weight", True, ar(128), ar(3) + [-1] * 29)}
         for i in (1, 2, 3, 4, 6, 7):
             plan[f"fwd{i}"] = (f"pts_linears.{i}.weight", False, ar(256), ar(256))
             plan[f"bwd{i}"] = (f"pts_linears.{i}.weight", True, ar(256), ar(256))
@@ -151,19 +153,22 @@ def _packs_for(params, device):
 
 
 def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, rw=None,
-           amax=None, bits_out=None, mask_bits=None):
+           amax=None, bits_out=None, mask_bits=None, head=None):
     """One nerf_x3_layer launch; amax (a device float, >= 0) is raised to max |C|.
     bits_out (int16 words, relu only) receives the ReLU mask of C as bits;
-    mask_bits (such words, instead of mask) masks C (nerf_x3_layer_bits)."""
-    if bits_out is None and mask_bits is None:
+    mask_bits (such words, instead of mask) masks C; head = (W [n, 16 mt], b [n],
+    out [P, 4], column): out[:, column:column + n] = C^T W^T + b
+    (nerf_x3_layer_ex)."""
+    if bits_out is None and mask_bits is None and head is None:
         call("nerf_x3_layer", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0),
              ptr(mask), mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu),
              ptr(C), C.stride(0), P, ptr(amax), _lib.stream_of(C.device))
         return
-    call("nerf_x3_layer_bits", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0),
+    hw, hb, hout, hcol = head if head is not None else (None, None, None, 0)
+    call("nerf_x3_layer_ex", ptr(wp), ptr(sw), mt, nk, ptr(bias), ptr(B), B.stride(0),
          ptr(mask), mask.stride(0) if mask is not None else 0, ptr(ru), ptr(rw), int(relu),
-         ptr(C), C.stride(0), P, ptr(amax), ptr(bits_out), ptr(mask_bits),
-         _lib.stream_of(C.device))
+         ptr(C), C.stride(0), P, ptr(amax), ptr(bits_out), ptr(mask_bits), ptr(hw), ptr(hb),
+         hw.shape[0] if hw is not None else 0, ptr(hout), hcol, _lib.stream_of(C.device))
 
 
 def relu_bits_words(P, m_tiles):
@@ -338,14 +343,16 @@ class NerfMLPFn(torch.autograd.Function):
         # the ReLU masks of h0..h7 as bits for the dgrad launches (32 B per sample
         # and layer instead of re-reading the 1 KiB of FP32 activations)
         bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
+        raw = torch.empty((P, 4), device=dev, dtype=f32)   # heads write straight into it
         for i in range(8):
             wp, sw, mt, nk = pk[f"fwd{i}"]
             B = E if i == 5 else src
             _layer(wp, sw, mt, nk, B, H[i], P, bias=p[f"pts_linears.{i}.bias"], relu=True,
-                   amax=amax[i:i + 1], bits_out=bits[i])
+                   amax=amax[i:i + 1], bits_out=bits[i],
+                   head=((p["alpha_linear.weight"], p["alpha_linear.bias"], raw, 3)
+                         if i == 7 else None))                  # NET:61 alpha on h7
             src = H[i]
         h7 = H[7]
-        alpha = torch.addmm(p["alpha_linear.bias"][:, None], p["alpha_linear.weight"], h7)  # [1,P]
         V = _act(288, P, dev)           # cat(feature, views enc)
         V[283:].zero_()                                            # feature rows: its layer
         wf, swf, mt, nk = pk["fwd_feat"]
@@ -354,18 +361,18 @@ class NerfMLPFn(torch.autograd.Function):
         _encode(dirs.detach().contiguous(), DIR_FREQS, V[256:283], amax[10:11])
         wv, swv, mt, nk = pk["fwd_views"]
         HV = _act(128, P, dev)
+        bits_v = torch.empty((relu_bits_words(P, 8),), device=dev, dtype=torch.int16)
         _layer(wv, swv, mt, nk, V, HV, P, bias=p["views_linears.0.bias"], relu=True,
-               amax=amax[11:12])
-        rgb = torch.addmm(p["rgb_linear.bias"][:, None], p["rgb_linear.weight"], HV)       # [3,P]
-        raw = torch.cat([rgb, alpha], 0).t().contiguous()
-        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, *params)
+               amax=amax[11:12], bits_out=bits_v,
+               head=(p["rgb_linear.weight"], p["rgb_linear.bias"], raw, 0))   # NET:68-70
+        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
         ctx.pts_grad = pts.requires_grad
         ctx.packs = pk
         return raw
 
     @staticmethod
     def backward(ctx, d_raw):
-        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, *params = ctx.saved_tensors
+        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, bits_v, *params = ctx.saved_tensors
         H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
         p = dict(zip(PARAM_NAMES, params))
         pk = ctx.packs
@@ -373,17 +380,21 @@ class NerfMLPFn(torch.autograd.Function):
         P = d_raw.shape[0]
         f32 = torch.float32
         grads = {}
-        d_raw = d_raw.t().contiguous()                              # [4, P]
-        d_rgb, d_sig = d_raw[0:3], d_raw[3:4]
+        DR = torch.zeros((32, P), device=dev, dtype=f32)   # d_raw^T: the K step of d hv
+        DR[:4].copy_(d_raw.t())
+        d_rgb, d_sig = DR[0:3], DR[3:4]
         wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
         post = {}              # slot -> (weight name, bias name or None, column fix-up)
         post[wb.add(d_rgb, HV, amax_b=amax[11:12])] = ("rgb_linear.weight", None, None)
         grads["rgb_linear.bias"] = d_rgb.sum(1)
-        d_hv = (p["rgb_linear.weight"].t() @ d_rgb) * (HV > 0)      # [128, P]
-        wv = p["views_linears.0.weight"]                            # [128, 283]
-        post[wb.add(d_hv, V, amax_b=torch.maximum(amax[8:9], amax[10:11]), with_bias=True)] = (
+        dmax = torch.zeros(11, device=dev, dtype=f32)   # max |d| of each layer-kernel output
+        # d hv = (W_rgb^T d_rgb) * (hv > 0): the views layer's ReLU bits
+        d_hv = _act(128, P, dev)
+        wrt, swrt, mt, nk = pk["bwd_rgb"]
+        _layer(wrt, swrt, mt, nk, DR, d_hv, P, mask_bits=bits_v, amax=dmax[10:11])
+        post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[8:9], amax[10:11]),
+                    with_bias=True)] = (
             "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
-        dmax = torch.zeros(10, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
         wvt, swvt, mt, nk = pk["bwd_views"]
         DF = _act(256, P, dev)
