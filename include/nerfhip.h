@@ -174,33 +174,6 @@ int nerf_x3_layer_ex(const float* w_packed, const int* w_scale, int m_tiles, int
                      int64_t ldc, int64_t P, float* amax_out, unsigned short* relu_bits,
                      const unsigned short* mask_bits, const float* head_w, const float* head_b,
                      int n_head, float* head_out, int head_col, nerf_stream_t stream);
-/* nerf_x3_chain: n_layers (2..5) consecutive 256 -> 256 layers with bias +
- *   ReLU in one launch, activations passed between layers in registers (the
- *   inference kernel's dataflow): layer 0 reads B (k_steps0 = 2 or 8 K steps,
- *   natural row order, row stride ldb); each layer l writes C[l] (row stride
- *   ldc[l]), its ReLU bits (nerf_x3_layer_ex layout, m_tiles 16) and raises
- *   amax[l] (nullable). slices: the layers' packed W one after another (layer 0
- *   in natural K order, layers l > 0 with the accumulator-order K permutation
- *   of nerfhip.train_mlp). Optional head on the last layer as in
- *   nerf_x3_layer_ex. Instances: (k_steps0, n_layers) in {(2, 5), (8, 2),
- *   (8, 3)}; others return NERF_E_UNSUPPORTED. */
-typedef struct NerfX3Chain {
-  const float* slices;
-  const int* w_scale[5];
-  const float* bias[5];
-  float* C[5];
-  int64_t ldc[5];
-  unsigned short* bits[5];
-  float* amax[5];
-  const float* B;
-  int64_t ldb;
-  int64_t P;
-  const float* head_w;
-  const float* head_b;
-  float* head_out;
-  int n_layers, k_steps0, n_head, head_col;
-} NerfX3Chain;
-int nerf_x3_chain(const NerfX3Chain* chain, nerf_stream_t stream);
 int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                   int64_t P, int64_t chunk, const float* amax_a, const float* amax_b,
                   float* part, float* bias_part, nerf_stream_t stream);

@@ -1338,325 +1338,6 @@ extern "C" int nerf_mlp_forward_x3_list(const float* w_slices, const float* w_he
   return check_launch("mlp_x3_kernel");
 }
 
-// Forward chain (C3): NL consecutive 256-row layers with bias + ReLU, their
-// activations handed from one layer to the next in registers, as in the
-// inference kernel. Layer 0 reads its input (NK0 K steps, natural row order)
-// from HBM; layer l > 0 takes layer l-1's ReLU output straight from the
-// accumulators (its W packed with the accumulator-order K permutation: slot j
-// of lane group g in K step q = row 16 (2q + j / 4) + 4 g + j % 4, see
-// nerfhip.train_mlp.X3Packer). Every layer still writes its output (FP32,
-// feature-major: the weight gradients read it), its ReLU bits and max |.|;
-// what the chain saves is re-reading 1 KiB per sample of each layer's input.
-// The weight slices of all layers are one contiguous stream (NK0 + 8 (NL-1)
-// per tile), staged like x3_layer_kernel's; the next tile's input is loaded
-// into the registers the last layer's slices free.
-constexpr int kMaxChain = 5;
-struct ChainArgs {
-  const uint4* slices;
-  const int* sw[kMaxChain];
-  const float* bias[kMaxChain];
-  float* C[kMaxChain];
-  int64_t ldc[kMaxChain];
-  unsigned short* bits[kMaxChain];
-  float* amax[kMaxChain];
-  const float* B;
-  int64_t ldb;
-  int64_t P;
-  const float* head_w;   // head on the last layer (nullable): as nerf_x3_layer_ex
-  const float* head_b;
-  int n_head;
-  float* head_out;
-  int head_col;
-};
-
-// s_waitcnt vmcnt(min(63, N)) for a wave-uniform N in [0, 127]
-__device__ __forceinline__ void vm_wait_upto(int n) {
-  switch (n >= 63 ? 63 : (n & 63)) {
-#define NERF_VMW(K) case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
-    NERF_VMW(0) NERF_VMW(1) NERF_VMW(2) NERF_VMW(3) NERF_VMW(4) NERF_VMW(5) NERF_VMW(6)
-    NERF_VMW(7) NERF_VMW(8) NERF_VMW(9) NERF_VMW(10) NERF_VMW(11) NERF_VMW(12) NERF_VMW(13)
-    NERF_VMW(14) NERF_VMW(15) NERF_VMW(16) NERF_VMW(17) NERF_VMW(18) NERF_VMW(19)
-    NERF_VMW(20) NERF_VMW(21) NERF_VMW(22) NERF_VMW(23) NERF_VMW(24) NERF_VMW(25)
-    NERF_VMW(26) NERF_VMW(27) NERF_VMW(28) NERF_VMW(29) NERF_VMW(30) NERF_VMW(31)
-    NERF_VMW(32) NERF_VMW(33) NERF_VMW(34) NERF_VMW(35) NERF_VMW(36) NERF_VMW(37)
-    NERF_VMW(38) NERF_VMW(39) NERF_VMW(40) NERF_VMW(41) NERF_VMW(42) NERF_VMW(43)
-    NERF_VMW(44) NERF_VMW(45) NERF_VMW(46) NERF_VMW(47) NERF_VMW(48) NERF_VMW(49)
-    NERF_VMW(50) NERF_VMW(51) NERF_VMW(52) NERF_VMW(53) NERF_VMW(54) NERF_VMW(55)
-    NERF_VMW(56) NERF_VMW(57) NERF_VMW(58) NERF_VMW(59) NERF_VMW(60) NERF_VMW(61)
-    NERF_VMW(62) NERF_VMW(63)
-#undef NERF_VMW
-  }
-}
-
-// Slice position k within a chain tile: layer L = chain_layer(k), K step
-// k - chain_off(L); what each slice issues after its weight pieces (the B
-// prefetch of the next tile in the last layer, the epilogue's 64 stores of C
-// after a layer's last slice) decides how many VMEM operations are younger
-// than the pieces of slice k+1 when slice k ends (those were staged at the
-// start of slice k-2).
-template <int NK0>
-__host__ __device__ constexpr int chain_off(int L) { return L == 0 ? 0 : NK0 + 8 * (L - 1); }
-template <int NK0>
-__host__ __device__ constexpr int chain_nk(int L) { return L == 0 ? NK0 : 8; }
-template <int NK0, int NL>
-__host__ __device__ constexpr int chain_layer(int k) {
-  int L = 0;
-  while (L + 1 < NL && k >= chain_off<NK0>(L + 1)) ++L;
-  return L;
-}
-template <int NK0, int NL>
-__host__ __device__ constexpr bool chain_last_of_layer(int k) {
-  return k == chain_off<NK0>(chain_layer<NK0, NL>(k)) + chain_nk<NK0>(chain_layer<NK0, NL>(k)) - 1;
-}
-// B prefetch loads (8 per K step) issued in slice k when the next tile exists
-template <int NK0, int NL>
-__host__ __device__ constexpr int chain_pf(int k) {
-  return (k >= 0 && chain_layer<NK0, NL>(k) == NL - 1 && k - chain_off<NK0>(NL - 1) < NK0) ? 8 : 0;
-}
-template <int NK0, int NL>
-__host__ __device__ constexpr int chain_stores(int k) {   // epilogue stores after slice k
-  return (k >= 0 && chain_last_of_layer<NK0, NL>(k)) ? 64 : 0;
-}
-
-struct ChainCtx {
-  uint4* ring;
-  __amdgpu_buffer_rsrc_t rW, rB;
-  int total, lane, wave, g4;
-  unsigned ldb4;
-  int nbB;
-};
-
-template <int NK0, int NL, int L>
-__device__ __forceinline__ void chain_layer_step(const ChainArgs& a, const ChainCtx& c, Op (&b)[8],
-                                                 int& g, int64_t tile, int64_t p, bool valid,
-                                                 bool has_next, unsigned von,
-                                                 float (&omax)[NL]) {
-  if constexpr (L < NL) {
-    constexpr int MT = 16, kSliceU4 = 2 * MT * 64, kPpw = 4;
-    constexpr int kTileSlices = NK0 + 8 * (NL - 1);
-    constexpr int nk = chain_nk<NK0>(L);
-    constexpr bool last = L == NL - 1;
-    __builtin_amdgcn_sched_barrier(0);   // no scheduling across layers (register pressure)
-    float mx = 0.0f;
-#pragma unroll
-    for (int q = 0; q < nk; ++q) mx = fmaxf(mx, op_absmax(b[q]));
-    const int e = act_exponent(sample_max(mx));
-    const float s = ldexpf(1.0f, e);
-#pragma unroll
-    for (int q = 0; q < nk; ++q) split_op(b[q], s);
-
-    f32x4 acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = f32x4(0.0f);
-#pragma unroll
-    for (int q = 0; q < nk; ++q) {
-      const int k = chain_off<NK0>(L) + q;   // this slice's position in the tile
-      // opaque stream position: otherwise every ring-slot address is computed
-      // once, ahead of the tile loop, and lives (spilled) through it
-      int go = g;
-      asm volatile("" : "+s"(go));
-      {   // stage slice g + 3 of the stream
-        const int gs = go + 3;
-        if (gs < c.total) {
-          const int qs = gs % kTileSlices;
-#pragma unroll
-          for (int i = 0; i < kPpw; ++i) {
-            const int bb = c.wave + 8 * i;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                c.rW, (lds_ptr_t)(c.ring + (gs & 3) * kSliceU4 + bb * 64), 16, (bb * 64 + c.lane) * 16,
-                __builtin_amdgcn_readfirstlane(qs * kSliceU4 * 16), 0, 0);
-          }
-        }
-      }
-      const unsigned base = lds_base((const float*)(c.ring + (go & 3) * kSliceU4), c.lane);
-      Frags x, y;
-      load_frags<0>(x, base);
-      layer_groups<0, MT / 2>(acc, base, b[q], x, y);
-      if (last && q < NK0) {   // the next tile's input into the freed registers
-        if (has_next) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            b[q][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                    c.rB, (int)(von + j * c.ldb4),
-                                                    (int)(32u * q * c.ldb4), 0));
-        }
-      }
-      if (g + 1 < c.total) {
-        // younger than slice g+1's pieces (staged in slice k-2): the pieces of
-        // g+2 and g+3, the prefetch loads and epilogue stores issued since
-        const int stat_pf = chain_pf<NK0, NL>(k - 2) + chain_pf<NK0, NL>(k - 1) + chain_pf<NK0, NL>(k);
-        const int stat_st = chain_stores<NK0, NL>(k - 2) + chain_stores<NK0, NL>(k - 1);
-        const int n = kPpw * ((g + 2 < c.total) + (g + 3 < c.total)) + (has_next ? stat_pf : 0) +
-                      stat_st;
-        vm_wait_upto(n);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      ++g;
-    }
-
-    __builtin_amdgcn_sched_barrier(0);
-    // the layer's kernel arguments read here, through an opaque index: hoisted
-    // out of the tile loop, all layers' pointers would stay live in SGPRs
-    int li = L;
-    asm volatile("" : "+s"(li));
-    const float inv = ldexpf(1.0f, -(*a.sw[li] + e));
-    const int64_t ldc = a.ldc[li];
-    const unsigned ldc4 = (unsigned)ldc * 4u;
-    const int nbC = (int)(16 * MT * ldc * 4);
-    const __amdgpu_buffer_rsrc_t rC =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.C[li], 0, nbC, 0x00020000);
-    unsigned voc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      voc[r] = valid ? (unsigned)(((int64_t)(4 * c.g4 + r) * ldc + p) * 4) : (unsigned)nbC;
-    const float* bias = a.bias[li];
-    unsigned short* bits = a.bits[li];
-    float hpart[3] = {0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int u0 = 0; u0 < MT; u0 += 4) {
-      const int64_t wb = (((tile * 8 + c.wave) * MT + u0) / 4) * 64 + c.lane;
-      // v[t][r] = the ReLU output of tile u0 + t, register r; for a non-last layer
-      // it lives in its slot of the next layer's B operand (K step u0/2 + t/2,
-      // slot 4 (t & 1) + r), so the stores read the registers the next layer uses
-      float vl[4][4];
-#define NERF_VGET(t, r) (last ? vl[t][r] : b[u0 / 2 + (t) / 2][4 * ((t) & 1) + (r)])
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {   // the power-of-two product is exact: one rounding, as + bias
-          const float val = fmaxf(acc[u0 + t][r] * inv + bias[16 * (u0 + t) + 4 * c.g4 + r], 0.0f);
-          if constexpr (last) vl[t][r] = val;
-          else b[u0 / 2 + t / 2][4 * (t & 1) + r] = val;
-        }
-      unsigned mine = 0u;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mine |= min(__float_as_uint(NERF_VGET(t, r)), 1u) << (4 * t + r);
-      if (valid) bits[wb] = (unsigned short)mine;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, NERF_VGET(t, r)), rC,
-                                                (int)voc[r], (int)(16u * (u0 + t) * ldc4), 0);
-          omax[L] = valid ? fmaxf(omax[L], NERF_VGET(t, r)) : omax[L];
-        }
-      if constexpr (last) {
-        if (a.head_out) {
-#pragma unroll
-          for (int cc = 0; cc < 3; ++cc) {
-            if (cc < a.n_head) {
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                const float4 hw = *reinterpret_cast<const float4*>(
-                    a.head_w + cc * 16 * MT + 16 * (u0 + t) + 4 * c.g4);
-                hpart[cc] = __builtin_fmaf(NERF_VGET(t, 0), hw.x, hpart[cc]);
-                hpart[cc] = __builtin_fmaf(NERF_VGET(t, 1), hw.y, hpart[cc]);
-                hpart[cc] = __builtin_fmaf(NERF_VGET(t, 2), hw.z, hpart[cc]);
-                hpart[cc] = __builtin_fmaf(NERF_VGET(t, 3), hw.w, hpart[cc]);
-              }
-            }
-          }
-        }
-      }
-#undef NERF_VGET
-    }
-    if constexpr (last) {
-      if (a.head_out) {
-#pragma unroll
-        for (int cc = 0; cc < 3; ++cc) {
-          if (cc < a.n_head) {
-            const float h = quad_sum(hpart[cc]) + a.head_b[cc];
-            if (valid && c.g4 == 0) a.head_out[p * 4 + a.head_col + cc] = h;
-          }
-        }
-      }
-    }
-    chain_layer_step<NK0, NL, L + 1>(a, c, b, g, tile, p, valid, has_next, von, omax);
-  }
-}
-
-template <int NK0, int NL>
-__global__ __launch_bounds__(kTrainThreads, 2) void x3_chain_kernel(const ChainArgs a) {
-  constexpr int kSliceU4 = 32 * 64;
-  constexpr int kTileSlices = NK0 + 8 * (NL - 1);
-  static_assert(NK0 <= 8 && NL >= 2 && NL <= kMaxChain, "chain shape");
-  __shared__ __attribute__((aligned(16))) uint4 ring[4 * kSliceU4];
-  ChainCtx c;
-  c.ring = ring;
-  c.lane = threadIdx.x & 63;
-  c.wave = threadIdx.x >> 6;
-  c.g4 = c.lane >> 4;
-  const int64_t P = a.P;
-  const int64_t ntiles = (P + kTrainTile - 1) / kTrainTile;
-  const int64_t t0 = blockIdx.x, tstride = gridDim.x;
-  const int nt = t0 < ntiles ? (int)((ntiles - 1 - t0) / tstride + 1) : 0;
-  c.total = nt * kTileSlices;
-  c.rW = __builtin_amdgcn_make_buffer_rsrc((void*)a.slices, 0, kTileSlices * kSliceU4 * 16,
-                                           0x00020000);
-  for (int gs = 0; gs < 3; ++gs) {   // prologue: slices 0..2
-    if (gs < c.total) {
-      const int qs = gs % kTileSlices;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int bb = c.wave + 8 * i;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            c.rW, (lds_ptr_t)(ring + (gs & 3) * kSliceU4 + bb * 64), 16, (bb * 64 + c.lane) * 16,
-            __builtin_amdgcn_readfirstlane(qs * kSliceU4 * 16), 0, 0);
-      }
-    }
-  }
-  auto sample_of = [&](int64_t tile) {
-    return tile * kTrainTile + c.wave * 16 + (c.lane & 15);
-  };
-  const int64_t ldb = a.ldb;
-  c.nbB = (int)(32 * NK0 * ldb * 4);
-  c.rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, c.nbB, 0x00020000);
-  c.ldb4 = (unsigned)ldb * 4u;
-  auto voff_b = [&](int64_t p, unsigned (&o)[8]) {
-    const unsigned base = p < P ? (unsigned)(((int64_t)8 * c.g4 * ldb + p) * 4) : (unsigned)c.nbB;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = base + (unsigned)j * c.ldb4;
-  };
-  Op b[8];
-  {
-    unsigned vo[8];
-    voff_b(sample_of(t0), vo);
-#pragma unroll
-    for (int q = 0; q < NK0; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        b[q][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                c.rB, (int)vo[j], (int)(32u * q * c.ldb4), 0));
-  }
-  __syncthreads();   // prologue slices landed (hipcc waits vmcnt(0) before the barrier)
-
-  float omax[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) omax[l] = 0.0f;
-  int g = 0;
-  for (int it = 0; it < nt; ++it) {
-    const int64_t tile = t0 + (int64_t)it * tstride;
-    const int64_t p = sample_of(tile);
-    const bool valid = p < P;
-    const bool has_next = it + 1 < nt;
-    const int64_t pn = sample_of(tile + tstride);
-    const unsigned von = pn < P ? (unsigned)(((int64_t)8 * c.g4 * ldb + pn) * 4) : (unsigned)c.nbB;
-    chain_layer_step<NK0, NL, 0>(a, c, b, g, tile, p, valid, has_next, von, omax);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile starts clean
-  }
-  __shared__ unsigned wg_max[kMaxChain];
-  if (threadIdx.x < NL) wg_max[threadIdx.x] = 0u;
-  __syncthreads();
-#pragma unroll
-  for (int l = 0; l < NL; ++l) atomicMax(&wg_max[l], __float_as_uint(omax[l]));
-  __syncthreads();
-  if (threadIdx.x < NL && a.amax[threadIdx.x])
-    atomicMax(reinterpret_cast<unsigned*>(a.amax[threadIdx.x]), wg_max[threadIdx.x]);
-}
-
 template <int MT, int NK, int EPI>
 static int launch_layer(const float* w, const int* sw, const float* bias, const float* B,
                         int64_t ldb, const float* mask, int64_t ldm, const float* ru,
@@ -1744,56 +1425,6 @@ static bool wgrad_dma_ok(const float* A, int64_t lda, int M, const float* B, int
   return P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
          ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
          (int64_t)M * lda * 4 < ((int64_t)1 << 31) && (int64_t)N * ldb * 4 < ((int64_t)1 << 31);
-}
-
-extern "C" int nerf_x3_chain(const NerfX3Chain* c, nerf_stream_t stream) {
-  NERF_REQUIRE(c && c->slices && c->B && c->n_layers >= 2 && c->n_layers <= kMaxChain &&
-                   (c->k_steps0 == 2 || c->k_steps0 == 8) && c->P >= 0 && c->ldb >= c->P,
-               "nerf_x3_chain: bad arguments");
-  NERF_REQUIRE(((uintptr_t)c->slices & 15) == 0, "nerf_x3_chain: packed W must be 16-byte aligned");
-  NERF_REQUIRE(!c->head_out || (c->head_w && c->head_b && c->n_head >= 1 && c->n_head <= 3 &&
-                                c->head_col >= 0 && c->head_col + c->n_head <= 4 &&
-                                ((uintptr_t)c->head_w & 15) == 0),
-               "nerf_x3_chain: bad head");
-  ChainArgs a;
-  for (int l = 0; l < kMaxChain; ++l) {
-    const bool on = l < c->n_layers;
-    if (on)
-      NERF_REQUIRE(c->w_scale[l] && c->bias[l] && c->C[l] && c->ldc[l] >= c->P && c->bits[l] &&
-                       ((uintptr_t)c->bits[l] & 1) == 0 &&
-                       256ll * c->ldc[l] * 4 < (1ll << 31),
-                   "nerf_x3_chain: bad layer");
-    a.sw[l] = on ? c->w_scale[l] : nullptr;
-    a.bias[l] = on ? c->bias[l] : nullptr;
-    a.C[l] = on ? c->C[l] : nullptr;
-    a.ldc[l] = on ? c->ldc[l] : 0;
-    a.bits[l] = on ? c->bits[l] : nullptr;
-    a.amax[l] = on ? c->amax[l] : nullptr;
-  }
-  NERF_REQUIRE(32ll * c->k_steps0 * c->ldb * 4 < (1ll << 31), "nerf_x3_chain: input spans 2 GiB");
-  NERF_REQUIRE(cdiv(c->P, kTrainTile) < (1ll << 31), "nerf_x3_chain: too many samples");
-  if (c->P == 0) return 0;
-  a.slices = (const uint4*)c->slices;
-  a.B = c->B;
-  a.ldb = c->ldb;
-  a.P = c->P;
-  a.head_w = c->head_w;
-  a.head_b = c->head_b;
-  a.n_head = c->n_head;
-  a.head_out = c->head_out;
-  a.head_col = c->head_col;
-  const int64_t tiles = cdiv(c->P, kTrainTile);
-  const int n_cu = stream_cu_count(stream);
-  const dim3 grid((unsigned)(tiles < n_cu ? tiles : n_cu));
-#define NERF_CHAIN(NK0, NL)                                                                  \
-  if (c->k_steps0 == NK0 && c->n_layers == NL) {                                             \
-    hipLaunchKernelGGL((x3_chain_kernel<NK0, NL>), grid, dim3(kTrainThreads), 0,             \
-                       as_stream(stream), a);                                                \
-    return check_launch("x3_chain_kernel");                                                  \
-  }
-  NERF_CHAIN(2, 5) NERF_CHAIN(8, 2) NERF_CHAIN(8, 3)
-#undef NERF_CHAIN
-  return fail(NERF_E_UNSUPPORTED, "nerf_x3_chain: unsupported (k_steps0, n_layers)");
 }
 
 extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb,

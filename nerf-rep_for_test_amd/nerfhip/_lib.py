@@ -34,7 +34,6 @@ SIGNATURES = {
                               _I64, _P, _P, _P, _P, _P, _I, _P, _I, _S]),
     "nerf_sum_partials": (_I, [_P, _I64, _I64, _P, _S]),
     "nerf_x3_wgrad_batch": (_I, [_P, _I, _I, _S]),
-    "nerf_x3_chain": (_I, [_P, _S]),
     "nerf_x3_wgrad": (_I, [_P, _I64, _I, _P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _S]),
     "nerf_x3_pack": (_I, [_P, _I, _S]),
     "nerf_composite_train_fwd": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _S]),

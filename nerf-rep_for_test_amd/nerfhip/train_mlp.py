@@ -171,54 +171,6 @@ def _layer(wp, sw, mt, nk, B, C, P, bias=None, relu=False, mask=None, ru=None, r
          hw.shape[0] if hw is not None else 0, ptr(hout), hcol, _lib.stream_of(C.device))
 
 
-def chain_perm(K=256):
-    """Column order of a layer fed by nerf_x3_chain from registers: packed
-    natural index 32q + 8g + j takes the input row 16 (2q + j // 4) + 4 g + j % 4
-    (the accumulator layout of the previous layer, csrc/mlp_x3.hip)."""
-    cols = []
-    for q in range(K // 32):
-        for g in range(4):
-            for j in range(8):
-                cols.append(16 * (2 * q + j // 4) + 4 * g + j % 4)
-    return cols
-
-
-class _ChainDesc(ctypes.Structure):
-    """NerfX3Chain (include/nerfhip.h)."""
-    _fields_ = [("slices", ctypes.c_void_p), ("w_scale", ctypes.c_void_p * 5),
-                ("bias", ctypes.c_void_p * 5), ("C", ctypes.c_void_p * 5),
-                ("ldc", ctypes.c_int64 * 5), ("bits", ctypes.c_void_p * 5),
-                ("amax", ctypes.c_void_p * 5), ("B", ctypes.c_void_p), ("ldb", ctypes.c_int64),
-                ("P", ctypes.c_int64), ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_void_p),
-                ("head_out", ctypes.c_void_p), ("n_layers", ctypes.c_int),
-                ("k_steps0", ctypes.c_int), ("n_head", ctypes.c_int), ("head_col", ctypes.c_int)]
-
-
-def _chain(slices, sws, biases, B, Cs, bits, P, amaxes, head=None):
-    """One nerf_x3_chain launch: len(Cs) layers, layer 0 reading B ([32 k0][P]
-    rows), outputs Cs[l] with ReLU bits bits[l] and max |.| into amaxes[l]."""
-    n = len(Cs)
-    d = _ChainDesc()
-    d.slices = slices.data_ptr()
-    for l in range(n):
-        d.w_scale[l] = sws[l].data_ptr()
-        d.bias[l] = biases[l].data_ptr()
-        d.C[l] = Cs[l].data_ptr()
-        d.ldc[l] = Cs[l].stride(0)
-        d.bits[l] = bits[l].data_ptr()
-        d.amax[l] = amaxes[l].data_ptr() if amaxes[l] is not None else None
-    d.B = B.data_ptr()
-    d.ldb = B.stride(0)
-    d.P = P
-    d.n_layers = n
-    d.k_steps0 = B.shape[0] // 32
-    if head is not None:
-        hw, hb, hout, hcol = head
-        d.head_w, d.head_b, d.head_out = hw.data_ptr(), hb.data_ptr(), hout.data_ptr()
-        d.n_head, d.head_col = hw.shape[0], hcol
-    call("nerf_x3_chain", ctypes.addressof(d), _lib.stream_of(B.device))
-
-
 def relu_bits_words(P, m_tiles):
     """int16 words of one layer's ReLU mask (nerf_x3_layer_bits layout)."""
     return -(-P // 128) * 128 * m_tiles

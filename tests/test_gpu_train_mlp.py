@@ -295,53 +295,3 @@ def test_x3_wgrad_batch_matches_matmul(dev):
             if bias:
                 rb = A.double().sum(1)
                 assert (gb.double() - rb).abs().max().item() / A.double().abs().sum(1).max().item() < 1e-6
-
-
-@pytest.mark.parametrize("k0,nl", [(8, 2), (8, 3), (2, 5)])
-def test_x3_chain_matches_layer_launches(dev, k0, nl):
-    """nerf_x3_chain (activations handed between layers in registers, later
-    layers packed in the accumulator-order K permutation) against the same
-    layers as separate nerf_x3_layer_ex launches: outputs within the FP32
-    summation-order bound, ReLU bits and max |.| equal; ragged P; the head on
-    the last layer."""
-    from nerfhip.train_mlp import (_chain, _layer, chain_perm, pack_x3_matrix, relu_bits_words)
-    g = torch.Generator(device=dev).manual_seed(21)
-    for P in (777, 4096):
-        K0 = 32 * k0
-        Ws = [torch.randn((256, K0 if l == 0 else 256), device=dev, generator=g) * (0.9 / (K0 if l == 0 else 256) ** 0.5)
-              for l in range(nl)]
-        bs = [torch.randn(256, device=dev, generator=g) * 0.1 for _ in range(nl)]
-        B = torch.randn((K0, P + 32), device=dev, generator=g)[:, :P]
-        hw = torch.randn((1, 256), device=dev, generator=g)
-        hb = torch.randn(1, device=dev, generator=g)
-        perm = chain_perm()
-        packs = [pack_x3_matrix(W if l == 0 else W[:, perm]) for l, W in enumerate(Ws)]
-        slices = torch.cat([pk for pk, _ in packs])
-        Cs = [torch.empty((256, P + 32), device=dev)[:, :P] for _ in range(nl)]
-        bits = [torch.empty(relu_bits_words(P, 16), device=dev, dtype=torch.int16) for _ in range(nl)]
-        am = [torch.zeros(1, device=dev) for _ in range(nl)]
-        raw = torch.zeros((P, 4), device=dev)
-        _chain(slices, [sw for _, sw in packs], bs, B, Cs, bits, P, am, head=(hw, hb, raw, 3))
-        # the same layers one launch each (natural packing)
-        src = B
-        raw2 = torch.zeros((P, 4), device=dev)
-        for l in range(nl):
-            wp, sw = pack_x3_matrix(Ws[l])
-            C2 = torch.empty((256, P), device=dev)
-            bt = torch.empty(relu_bits_words(P, 16), device=dev, dtype=torch.int16)
-            a2 = torch.zeros(1, device=dev)
-            _layer(wp, sw, 16, src.shape[0] // 32, src, C2, P, bias=bs[l], relu=True, amax=a2,
-                   bits_out=bt, head=(hw, hb, raw2, 3) if l == nl - 1 else None)
-            ref = C2.double()
-            scale = ref.abs().amax(0) + 1e-3
-            assert ((Cs[l].double() - ref).abs() / scale).max().item() < 1e-5, (l, P)
-            # bits of valid samples (words of invalid lanes are not written) may
-            # differ only where an output sits within rounding of 0
-            lane_sample = (torch.arange(bt.numel(), device=dev) // 256) * 16 + \
-                torch.arange(bt.numel(), device=dev) % 16
-            ok = lane_sample < P
-            differ = ((bits[l] != bt) & ok).sum().item()
-            assert differ <= max(1, bt.numel() // 1000), (l, differ)
-            assert abs(am[l].item() - a2.item()) <= 1e-5 * a2.item()
-            src = C2
-        assert ((raw[:, 3] - raw2[:, 3]).abs() / (raw2[:, 3].abs() + 1)).max().item() < 1e-5
