@@ -97,6 +97,9 @@ def main():
                     help="c3: replay the step as one HIP graph (capturable Adam) instead of "
                          "launching it op by op; the step is GPU-bound (~5.5 ms of kernel "
                          "time), the graph measured 0.15 ms slower (5.46 vs 5.32 ms)")
+    ap.add_argument("--ert-segment", type=int, default=8,
+                    help="c4: depth-segment length of the ERT sample compaction (8: 1.94 "
+                         "Mrays/s, 16: 1.92, 32: 1.86, 64: 1.70 measured)")
     ap.add_argument("--no-fp32-run", action="store_true",
                     help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
     args = ap.parse_args()
@@ -143,7 +146,7 @@ def main():
     def make_pipe(precision):
         pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
                             mlp_precision=precision, enable_ess=c4, enable_ert=c4,
-                            ert_threshold=0.01)
+                            ert_threshold=0.01, ert_segment=args.ert_segment)
         pipe.set_weights(params)
         if c4:
             pipe.set_grid(make_occupancy_grid(0, 128, 1.2, 0.1))
@@ -215,7 +218,7 @@ def main():
             "full_samples_per_ray": full / (rays / world),
             "evaluated_fraction": ev / max(1, full),
             "note": "MLP samples evaluated per ray (coarse 64 + fine 192 in full) with depth "
-                    "segments of 32 and rays retired at T < 0.01 (their later weights are "
+                    f"segments of {args.ert_segment} and rays retired at T < 0.01 (their later weights are "
                     "zeroed by _raw2outputs_with_ert, VR:1115-1123)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if c4:
