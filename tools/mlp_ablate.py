@@ -59,7 +59,12 @@ VARIANTS = {"base": [], "nobar": ["-DABL_NOBAR"], "nodma": ["-DABL_NODMA"],
             "x3_ilv1": ["-DMLP_X3_ILV=1"], "x3_ilv3": ["-DMLP_X3_ILV=3"],
             # workgroups of an XCD start staggered by k * N s_sleep(127) (k = 0..7)
             "x3_skew1": ["-DMLP_X3_SKEW=1"], "x3_skew2": ["-DMLP_X3_SKEW=2"],
-            "x3_skew3": ["-DMLP_X3_SKEW=3"]}
+            "x3_skew3": ["-DMLP_X3_SKEW=3"],
+            # order of the 6 products per tile pair (x3_ops.h MLP_X3_ORD; shipped 4)
+            "x3_ord0": ["-DMLP_X3_ORD=0"], "x3_ord1": ["-DMLP_X3_ORD=1"], "x3_ord2": ["-DMLP_X3_ORD=2"],
+            "x3_ord3": ["-DMLP_X3_ORD=3"], "x3_ord4": ["-DMLP_X3_ORD=4"],
+            "x3_ord5": ["-DMLP_X3_ORD=5"], "x3_ord7": ["-DMLP_X3_ORD=7"],
+            "x3_ord8": ["-DMLP_X3_ORD=8"]}
 
 
 def is_x3(v):
