@@ -698,27 +698,33 @@ using namespace nerfhip;
 // ---------------------------------------------------------------------------
 // Frequency encoding for the training MLP (freq.py:7-32), feature-major:
 // out[j][p] with j = c (raw coordinate), 3 + 6f + c (sin 2^f x_c), 6 + 6f + c
-// (cos 2^f x_c) -- the column order of torch.cat([x, sin, cos, ...], -1). One
-// thread per sample, so every output row is a coalesced store; the max |.| of
-// the block is raised into *amax (float bits as uint: all values are >= 0).
-// 2^f x is exact (power of two); sinf/cosf are the same device-library calls
-// torch's sin/cos kernels make.
+// (cos 2^f x_c) -- the column order of torch.cat([x, sin, cos, ...], -1). A
+// block is 64 samples x W waves, wave w taking the bands f = w, w + W, ...
+// (wave 0 also the raw coordinates), so every output row is a coalesced 256-B
+// store and the accurate sincosf calls of one sample (large arguments, up to
+// 2^9 x) run on W waves instead of one thread's chain (measured 30 -> see
+// DESIGN §6). The block's max |.| is raised into *amax once (float bits as
+// uint: all values are >= 0). 2^f x is exact (power of two); sinf/cosf are the
+// same device-library calls torch's sin/cos kernels make.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void freq_encode_fm_kernel(const float* __restrict__ x,
-                                                             int64_t ldx, int64_t P, int L,
-                                                             float* __restrict__ out, int64_t ldo,
-                                                             unsigned* __restrict__ amax) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+constexpr int kEncMaxWaves = 16;
+__global__ __launch_bounds__(64 * kEncMaxWaves) void freq_encode_fm_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t P, int L, float* __restrict__ out,
+    int64_t ldo, unsigned* __restrict__ amax) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * 64 + lane;
   float m = 0.0f;
   if (p < P) {
     float v[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       v[c] = x[p * ldx + c];
-      out[c * ldo + p] = v[c];
-      m = fmaxf(m, fabsf(v[c]));
+      if (wave == 0) {
+        out[c * ldo + p] = v[c];
+        m = fmaxf(m, fabsf(v[c]));
+      }
     }
-    for (int f = 0; f < L; ++f) {
+    for (int f = wave; f < L; f += nw) {
       const float k = (float)(1 << f);
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -732,9 +738,15 @@ __global__ __launch_bounds__(256) void freq_encode_fm_kernel(const float* __rest
     }
   }
   if (amax) {
+    __shared__ float wmax[kEncMaxWaves];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+    if (lane == 0) wmax[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < nw; ++w) m = fmaxf(m, wmax[w]);
+      atomicMax(amax, __float_as_uint(m));
+    }
   }
 }
 
@@ -903,7 +915,8 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
   NERF_REQUIRE(P >= 0 && ldx >= 3 && ldo >= P && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm: bad size");
   if (P == 0) return 0;
-  hipLaunchKernelGGL(freq_encode_fm_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
+  const int waves = n_freq < 1 ? 1 : (n_freq < kEncMaxWaves ? n_freq : kEncMaxWaves);
+  hipLaunchKernelGGL(freq_encode_fm_kernel, dim3((unsigned)cdiv(P, 64)), dim3(64 * waves), 0,
                      as_stream(stream), x, ldx, P, n_freq, out, ldo, (unsigned*)amax);
   return check_launch("freq_encode_fm_kernel");
 }

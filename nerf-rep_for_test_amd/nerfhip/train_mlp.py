@@ -385,8 +385,10 @@ class NerfMLPFn(torch.autograd.Function):
         d_rgb, d_sig = DR[0:3], DR[3:4]
         wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
         post = {}              # slot -> (weight name, bias name or None, column fix-up)
-        post[wb.add(d_rgb, HV, amax_b=amax[11:12])] = ("rgb_linear.weight", None, None)
-        grads["rgb_linear.bias"] = d_rgb.sum(1)
+        # the heads' bias gradients come out of the batched launch too (its row
+        # sums), not from separate reductions over P
+        post[wb.add(d_rgb, HV, amax_b=amax[11:12], with_bias=True)] = (
+            "rgb_linear.weight", "rgb_linear.bias", None)
         dmax = torch.zeros(11, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         # d hv = (W_rgb^T d_rgb) * (hv > 0): the views layer's ReLU bits
         d_hv = _act(128, P, dev)
@@ -401,8 +403,8 @@ class NerfMLPFn(torch.autograd.Function):
         _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
         post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
             "feature_linear.weight", "feature_linear.bias", None)
-        post[wb.add(d_sig, H[7], amax_b=amax[7:8])] = ("alpha_linear.weight", None, None)
-        grads["alpha_linear.bias"] = d_sig.sum(1)
+        post[wb.add(d_sig, H[7], amax_b=amax[7:8], with_bias=True)] = (
+            "alpha_linear.weight", "alpha_linear.bias", None)
         # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
         wft, swft, _, _ = pk["bwd_feat"]
         D = _act(256, P, dev)
