@@ -702,8 +702,8 @@ using namespace nerfhip;
 // block is 64 samples x W waves, wave w taking the bands f = w, w + W, ...
 // (wave 0 also the raw coordinates), so every output row is a coalesced 256-B
 // store and the accurate sincosf calls of one sample (large arguments, up to
-// 2^9 x) run on W waves instead of one thread's chain (measured 30 -> see
-// DESIGN §6). The block's max |.| is raised into *amax once (float bits as
+// 2^9 x) run on W waves instead of one thread's chain (C3 step: 122 -> 115 us
+// for the 4 launches). The block's max |.| is raised into *amax once (float bits as
 // uint: all values are >= 0). 2^f x is exact (power of two); sinf/cosf are the
 // same device-library calls torch's sin/cos kernels make.
 // ---------------------------------------------------------------------------
