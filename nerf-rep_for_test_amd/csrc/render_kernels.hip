@@ -505,10 +505,12 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
 #pragma unroll
   for (int q = 0; q < QN; ++q) x[q] = q < nq ? ur[t + FINE_LANES * q] : 0.0f;
   fine_search<true>(cdf, nb, x, pos);
+  int lo_rank[QN];   // below + 1: a lower bound of #{z <= x} for the sample (see the merge)
 #pragma unroll
   for (int q = 0; q < QN; ++q) {   // (queries q >= nq run on u = 0 and are never stored)
     const int inds = pos[q];
     const int below = inds - 1 > 0 ? inds - 1 : 0;
+    lo_rank[q] = below + 1;
     const int above = inds < nb - 1 ? inds : nb - 1;
     const float cg0 = cdf[below], cg1 = cdf[above];
     const float bg0 = 0.5f * (zc[below + 1] + zc[below]);
@@ -530,7 +532,8 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
   bool unsorted = false;
   for (int j = t; j + 1 < n_imp; j += FINE_LANES) unsorted |= zf[j] > zf[j + 1];
   const unsigned long long bal = __ballot(unsorted);
-  if ((bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull) {
+  const bool sorted_in_place = ((bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull) == 0;
+  if (!sorted_in_place) {
     for (int k = 2; k <= p2; k <<= 1) {
       for (int jj = k >> 1; jj > 0; jj >>= 1) {
         for (int i = t; i < p2; i += FINE_LANES) {
@@ -556,7 +559,22 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
 #pragma unroll
   for (int c = 0; c < CN; ++c) xc[c] = c < ncl ? zc[t + FINE_LANES * c] : 0.0f;
   fine_search<false>(zf, n_imp, xc, pcz);
-  fine_search<true>(zc, S, x, pos);
+  if (sorted_in_place) {
+    // #{z <= x} of a fine sample from its own bin instead of a search: x is
+    // bg0 + tt (bg1 - bg0) with tt >= 0 (cdf[below] <= u) and bg0 = the mid of
+    // z[below], z[below + 1] >= z[below] (float rounding is monotone), so the
+    // count is at least below + 1; a short forward walk (usually one or two
+    // reads) finds it exactly. Only while x is still the value its bin produced,
+    // i.e. when the ray's samples needed no sort (eval: sorted u).
+#pragma unroll
+    for (int q = 0; q < QN; ++q) {
+      int r = lo_rank[q];
+      while (r < S && zc[r] <= x[q]) ++r;
+      pos[q] = r;
+    }
+  } else {
+    fine_search<true>(zc, S, x, pos);
+  }
   if (!live) return;
   float* out = z_all + ray * (int64_t)(S + n_imp);
 #pragma unroll
