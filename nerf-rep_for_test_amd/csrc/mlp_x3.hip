@@ -707,7 +707,18 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
   // HBM operands as buffer resources: a lane's offset is one 32-bit VGPR, the
   // row offset an SGPR, and a sample past P reads 0 / drops its store (offset
   // pushed past num_records) -- no per-load address registers or branches
-  const int nbB = (int)(32 * NK * ldb * 4), nbC = (int)(16 * MT * ldc * 4);
+  // X3L_ABL_*: timing-only builds (tools/layer_ablate.sh) whose B loads or C
+  // stores are dropped by a zero-record descriptor; their outputs are wrong
+#if defined(X3L_ABL_NOLOAD)
+  const int nbB = 0;
+#else
+  const int nbB = (int)(32 * NK * ldb * 4);
+#endif
+#if defined(X3L_ABL_NOSTORE)
+  const int nbC = 0;
+#else
+  const int nbC = (int)(16 * MT * ldc * 4);
+#endif
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, nbC, 0x00020000);
   const int nbM = mask ? (int)(16 * MT * ldm * 4) : 0;
@@ -862,7 +873,9 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
         }
       }
     }
+#if !defined(X3L_ABL_NOWAIT)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile starts clean
+#endif
   }
   if (amax_out) {   // one atomic per workgroup (as ordered uint bits: values >= 0)
     __shared__ unsigned wg_max;
