@@ -93,6 +93,12 @@ def main():
     ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
                     help="c3: the MLPs on the x3 MFMA training kernels (default) or as torch "
                          "modules (FP32 hipBLASLt GEMMs)")
+    ap.add_argument("--train-launch", default="auto", choices=["auto", "eager", "graph"],
+                    help="c3: how a step's kernels are launched: op by op (eager), one HIP "
+                         "graph replay (graph), or (auto, 1 rank) whichever ran faster in a "
+                         "5-step calibration of each on this box before the timed steps "
+                         "(the step is GPU-bound on a fast host and launch-bound on a slow "
+                         "one: 5.33 ms of kernels ran 5.71 ms eager on one box)")
     ap.add_argument("--train-graph", action="store_true",
                     help="c3: replay the step as one HIP graph (capturable Adam) instead of "
                          "launching it op by op; the step is GPU-bound (~5.5 ms of kernel "
@@ -269,8 +275,9 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
     poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
     K = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32,
                      device=dev)
-    graph = args.train_graph
-    tr = NerfTrainer(dev, params, mlp=args.train_mlp, graph=graph)
+    launch = "graph" if args.train_graph else args.train_launch
+    if launch == "auto" and (world > 1 or args.train_mlp != "x3"):
+        launch = "eager"   # the graph step is calibrated on one rank with the HIP ops only
     group = dist.group.WORLD if world > 1 else None
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     nrays = 1024
@@ -283,11 +290,32 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
         return ro, rd, target
 
     n_steps = args.steps if steps is None else steps
-    n_warm = args.warmup if warmup is None else warmup
+    n_warm = max(3, args.warmup if warmup is None else warmup)   # the graph captures step 3
     batches = [batch() for _ in range(n_warm + n_steps)]
-    for i in range(n_warm):
-        tr.step(*batches[i], group=group)
-    torch.cuda.synchronize()
+
+    def warmed(graph):
+        tr = NerfTrainer(dev, params, mlp=args.train_mlp, graph=graph)
+        for i in range(n_warm):
+            tr.step(*batches[i], group=group)
+        torch.cuda.synchronize()
+        return tr
+
+    calib = None
+    if launch == "auto":
+        # 5 steps of each launch mode on this box (same batches, separate trainers);
+        # the timed steps below run the faster one from a fresh warm trainer state
+        calib = {}
+        for mode in ("eager", "graph"):
+            t = warmed(mode == "graph")
+            t0 = time.perf_counter()
+            for i in range(5):
+                t.step(*batches[n_warm + i], group=group)
+            torch.cuda.synchronize()
+            calib[mode] = (time.perf_counter() - t0) / 5 * 1e3
+            del t
+        launch = min(calib, key=calib.get)
+    graph = launch == "graph"
+    tr = warmed(graph)
     barrier()
     t0 = time.perf_counter()
     for i in range(n_steps):
@@ -313,8 +341,11 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
                                "rank, perturb 1, training-mode u, MSE coarse+fine, clip 40, Adam",
                    "baseline_config": "configs[2]", "N_rays": nrays, "N_samples": 64,
                    "N_importance": 128, "train_mlp": args.train_mlp,
-                   "step_launch": "one HIP graph replay per step (captured on the 3rd step)"
-                                  if graph else "eager (op-by-op launches)",
+                   "step_launch": ("one HIP graph replay per step (captured on the 3rd step)"
+                                   if graph else "eager (op-by-op launches)") +
+                                  (f"; chosen by a 5-step calibration (ms/step: eager "
+                                   f"{calib['eager']:.2f}, graph {calib['graph']:.2f})"
+                                   if calib else ""),
                    "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
         "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
