@@ -600,9 +600,14 @@ __device__ __forceinline__ void vm_wait_slices(int n_pieces) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The K step's groups; with nxt, the next K step's operand is split (FP32 ->
+// FP16 hi/lo at scale s, as split_op) in the MFMA shadows of the even groups,
+// 8 / NG value pairs each, into t, committed to *nxt after the last group (it
+// is not read by this K step). Same values as splitting it up front.
 template <int G, int NG>
 __device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op& b, Frags& x,
-                                             Frags& y) {
+                                             Frags& y, Op* nxt = nullptr, float s = 0.0f,
+                                             Op* t = nullptr) {
   if constexpr (G < NG) {
     lds_drain();
     if constexpr (G + 1 < NG) {
@@ -612,8 +617,30 @@ __device__ __forceinline__ void layer_groups(f32x4* acc, unsigned base, const Op
     __builtin_amdgcn_sched_barrier(0);
     if constexpr ((G & 1) == 0) mfma3x2<false>(acc[2 * G], acc[2 * G + 1], x, b);
     else mfma3x2<false>(acc[2 * G], acc[2 * G + 1], y, b);
+    if constexpr ((G & 1) == 0) {
+      constexpr int kPairs = 8 / NG;   // value pairs split after this group
+      if (nxt) {
+#pragma unroll
+        for (int i = 0; i < kPairs; ++i) {
+          constexpr int k0 = (G / 2) * kPairs;
+          float hp, lp;
+          split2((*nxt)[2 * (k0 + i)], (*nxt)[2 * (k0 + i) + 1], s, hp, lp);
+          asm volatile("" : "+v"(hp), "+v"(lp));
+          (*t)[k0 + i] = hp;
+          (*t)[4 + k0 + i] = lp;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // up to 2 VALU
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
-    layer_groups<G + 1, NG>(acc, base, b, x, y);
+    if constexpr (G + 1 == NG) {
+      if (nxt) *nxt = *t;
+    }
+    layer_groups<G + 1, NG>(acc, base, b, x, y, nxt, s, t);
   }
 }
 
@@ -764,8 +791,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
     for (int q = 0; q < NK; ++q) mx = fmaxf(mx, op_absmax(b[q]));
     const int e = act_exponent(sample_max(mx));
     const float s = ldexpf(1.0f, e);
-#pragma unroll
-    for (int q = 0; q < NK; ++q) split_op(b[q], s);
+    split_op(b[0], s);   // b[1..NK-1] in the MFMA shadows of the K loop
+    Op split_tmp;
 
     f32x4 acc[MT];
 #pragma unroll
@@ -777,7 +804,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
       const unsigned base = lds_base((const float*)(ring + (g & 3) * kSliceU4), lane);
       Frags x, y;
       load_frags<0>(x, base);
-      layer_groups<0, MT / 2>(acc, base, b[q], x, y);
+      if (q + 1 < NK) layer_groups<0, MT / 2>(acc, base, b[q], x, y, &b[q + 1], s, &split_tmp);
+      else layer_groups<0, MT / 2>(acc, base, b[q], x, y);
       if (has_next) load_b(q, von, b[q]);   // K step q of the next tile, registers just freed
       if (g + 1 < total) {   // slice g+1 landed (this wave's pieces), then visible to all
         if (q >= 2) {
