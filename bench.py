@@ -77,10 +77,14 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
                     help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
                          "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2: lego 800x800 64c+128f (BASELINE configs[1], the headline); "
                          "c3: train step, 1024 rays/rank (configs[2]); "
-                         "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99)")
+                         "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99); "
+                         "c5: the lego test set (the 25 packed views cycled, one per step; "
+                         "PSNR/SSIM over all of them from the sharded renders, configs[4])")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the C4 (ESS + ERT) sub-record of the default run")
     ap.add_argument("--checkpoint", default=None,
                     help="trained weights (a reference-format .pth or model dir); default: "
                          "checkpoints/lego (trained by tools/train_lego.py) when present")
@@ -112,7 +116,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nerfhip.dist import render_frame_sharded
+    from nerfhip.dist import render_frame_interleaved, render_frame_sharded
     from nerfhip.render import NerfPipeline
     from nerfhip.synthetic import make_occupancy_grid, make_params
 
@@ -146,30 +150,36 @@ def main():
             dist.barrier()
 
     c4 = args.config == "c4"
+    c5 = args.config == "c5"
     if args.config == "c3":
         return bench_train(args, world, rank, dev, params, data, barrier)
 
-    def make_pipe(precision):
+    def make_pipe(precision, ess_ert):
         pipe = NerfPipeline(dev, N_samples=64, N_importance=128, near=2.0, far=6.0,
-                            mlp_precision=precision, enable_ess=c4, enable_ert=c4,
+                            mlp_precision=precision, enable_ess=ess_ert, enable_ert=ess_ert,
                             ert_threshold=0.01, ert_segment=args.ert_segment)
         pipe.set_weights(params)
-        if c4:
+        if ess_ert:
             pipe.set_grid(make_occupancy_grid(0, 128, 1.2, 0.1))
         return pipe
 
-    def measure(precision):
+    def frame_fn(pipe, ess_ert):
+        """One sharded frame: C2 row bands; C4 2048-ray chunks dealt round-robin
+        (chunk c -> rank c mod P), grid self-updates replayed."""
+        def frame(pose, K):
+            if ess_ert:
+                return render_frame_interleaved(
+                    lambda cs: pipe.render_chunks(H, W, pose, K, cs), H, W, rank, world, dev)
+            return render_frame_sharded(lambda p0, n: pipe.render_band(H, W, pose, K, p0, n),
+                                        H, W, rank, world, dev)
+        return frame
+
+    def measure(precision, ess_ert, steps, warmup):
         """warmup + K timed frames (barrier + sync both sides, max over ranks)."""
-        pipe = make_pipe(precision)
-
-        def frame(i):
-            pose, K = lego_camera(H, W, i)
-            return render_frame_sharded(
-                lambda p0, n: pipe.render_band(H, W, pose, K, p0, n),
-                H, W, rank, world, dev, chunk_aligned=c4)
-
-        for i in range(args.warmup):
-            frame(i)
+        pipe = make_pipe(precision, ess_ert)
+        frame = frame_fn(pipe, ess_ert)
+        for i in range(warmup):
+            frame(*lego_camera(H, W, i))
         torch.cuda.synchronize()
         barrier()
         pipe.timer = []
@@ -177,8 +187,8 @@ def main():
         pipe.ert_stats = []
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            frame(args.warmup + i)
+        for i in range(steps):
+            frame(*lego_camera(H, W, warmup + i))
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -188,11 +198,12 @@ def main():
             elapsed = float(t.item())
         timer, pipe.timer = pipe.timer, None
         stages, pipe.stage_timer = pipe.stage_timer, None
-        roof = roofline(precision, timer, elapsed, world, H, W, pmc_workload=world == 1 and not c4)
-        roof["byte_kernels"] = byte_kernels(stages, args.steps)
+        roof = roofline(precision, timer, elapsed, world, H, W,
+                        pmc_workload=world == 1 and not ess_ert)
+        roof["byte_kernels"] = byte_kernels(stages, steps)
         return pipe, elapsed, roof
 
-    pipe, elapsed, roof = measure(args.precision)
+    pipe, elapsed, roof = measure(args.precision, c4, args.steps, args.warmup)
     rays = H * W * args.steps
     result = {
         "metric": METRIC,
@@ -207,42 +218,81 @@ def main():
         "vs_baseline": None,
         "dtype": DTYPES[args.precision],
         "data": data,
-        "config": {"workload": "lego 800x800, 64 coarse + 128 fine samples, 1 frame per step "
+        "config": {"workload": ("lego 800x800 test set (the 25 packed test views 0, 8, ..., 192 "
+                                "cycled), " if c5 else
+                                "lego 800x800, ") + "64 coarse + 128 fine samples, 1 frame per step "
                                "(test poses cycled), " +
                                ("ESS + ERT on (threshold 0.01, synthetic occupancy grid, "
                                 "2048-ray chunks)" if c4 else "ESS/ERT off") + ", perturb 0, eval",
-                   "baseline_config": "configs[3]" if c4 else "configs[1]",
+                   "baseline_config": {"c2": "configs[1]", "c4": "configs[3]",
+                                       "c5": "configs[4]"}[args.config],
                    "H": H, "W": W, "N_samples": 64, "N_importance": 128,
                    "mlp_precision": args.precision,
-                   "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
+                   "parallelism": (f"2048-ray chunks dealt round-robin x{world} (chunk c -> rank "
+                                   f"c mod {world}) + RCCL all-gather of pixels" if c4 else
+                                   f"row-band tiles x{world} + RCCL all-gather of pixels")},
         "roofline": roof,
     }
     if c4:
-        ev, full = pipe.evaluated_samples()
-        result["ert_compaction"] = {
-            "evaluated_samples_per_ray": ev / (rays / world),
-            "full_samples_per_ray": full / (rays / world),
-            "evaluated_fraction": ev / max(1, full),
-            "note": "MLP samples evaluated per ray (coarse 64 + fine 192 in full) with depth "
-                    f"segments of {args.ert_segment} and rays retired at T < 0.01 (their later weights are "
-                    "zeroed by _raw2outputs_with_ert, VR:1115-1123)"}
+        result["ert_compaction"] = ert_report(pipe, rays, world, args.ert_segment, dev)
+    cpu = host_cpus()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        torch.set_num_threads(cpu["threads_used"])
         if c4:
             result["cpu_baseline"], result["parity"] = cpu_baseline_c4(
-                make_pipe(args.precision), H, W, params, args.cpu_rows)
+                make_pipe(args.precision, True), H, W, params, args.cpu_rows, cpu)
         else:
             result["parity"] = oracle_parity(pipe, H, W, params, args.cpu_rows)
-            result["cpu_baseline"] = torch_cpu_baseline(pipe, H, W, params, 2 * args.cpu_rows,
+            result["cpu_baseline"] = torch_cpu_baseline(pipe, H, W, params, cpu,
                                                         result["parity"])
+            result["cpu_baseline_c1"] = torch_cpu_baseline_c1(params, cpu, dev)
         result["psnr_vs_ref"] = result["parity"]["psnr_fine_rgb"]
-    if rank == 0 and world == 1 and not c4 and not args.no_gt and os.path.exists(GT_PATH):
-        result["psnr_vs_gt"] = psnr_vs_gt(pipe, H, W, result.get("parity"))
+    if rank == 0 and world == 1 and not c5:
+        # the whole frame against the reference's OWN render of it (make_ref_frames.py)
+        if c4:
+            pipe_c4 = make_pipe(args.precision, True)
+            result["parity_vs_reference_frame"] = reference_frame_parity(
+                pipe_c4, "r2_c4_frame16", H, W, ckpt)
+            del pipe_c4
+        else:
+            result["parity_vs_reference_frame"] = reference_frame_parity(
+                pipe, "r0_c2_frame0", H, W, ckpt)
+    if (c5 or (world == 1 and not c4)) and not args.no_gt and os.path.exists(GT_PATH):
+        ev = testset_eval(frame_fn(pipe, c4), H, W, rank, result.get("parity"))
+        if rank == 0:
+            result["psnr_vs_gt"] = ev
     del pipe
-    if args.precision != "fp32" and not args.no_fp32_run:
-        _, el32, roof32 = measure("fp32")
+    if args.precision != "fp32" and not args.no_fp32_run and not c5:
+        _, el32, roof32 = measure("fp32", c4, args.steps, args.warmup)
         result["fp32_mfma"] = {"value": rays / el32 / 1e6, "ms_per_step": el32 / args.steps * 1e3,
                                "dtype": DTYPES["fp32"], "roofline": roof32}
-    if world == 1 and not c4 and not args.no_c3:
+    if args.config == "c2" and not args.no_c4:
+        # BASELINE configs[3] timed in the same run: ESS + ERT, interleaved chunks
+        torch.cuda.empty_cache()
+        c4_steps = max(1, min(args.steps, 5))
+        p4, el4, roof4 = measure(args.precision, True, c4_steps, 1)
+        rays4 = H * W * c4_steps
+        rec = {"metric": "Mrays/s + ms/frame, lego 800x800 (64c+128f) with ESS + ERT",
+               "value": rays4 / el4 / 1e6, "unit": "Mrays/s", "steps": c4_steps, "warmup": 1,
+               "ms_per_step": el4 / c4_steps * 1e3, "dtype": DTYPES[args.precision],
+               "config": {"workload": "lego 800x800, 64c+128f, ESS + ERT (threshold 0.01, "
+                                      "synthetic occupancy grid make_occupancy_grid(0, 128, 1.2, "
+                                      "0.1) self-updated by the reference's rule), perturb 0, "
+                                      "eval, 1 frame per step (test poses cycled)",
+                          "baseline_config": "configs[3]",
+                          "parallelism": f"2048-ray chunks round-robin x{world} + RCCL "
+                                         f"all-gather"},
+               "roofline": {k: roof4[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
+                                                  "avg_launch_ms", "launches")},
+               "ert_compaction": ert_report(p4, rays4, world, args.ert_segment, dev)}
+        del p4
+        if rank == 0 and world == 1:
+            p4 = make_pipe(args.precision, True)
+            rec["parity_vs_reference_frame"] = reference_frame_parity(
+                p4, "r2_c4_frame16", H, W, ckpt)
+            del p4
+        result["c4_ess_ert"] = rec
+    if world == 1 and args.config == "c2" and not args.no_c3:
         # the frames' multi-GB buffers are still cached by torch's allocator: give
         # them back before the 1024-ray step settles into its own working set
         torch.cuda.empty_cache()
@@ -254,6 +304,7 @@ def main():
     if "parity" in result:
         result["parity"].pop("_maps", None)
     if rank == 0:
+        result["host"] = cpu
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -483,14 +534,15 @@ def oracle_parity(pipe, H, W, params, rows):
     return par
 
 
-def torch_cpu_baseline(pipe, H, W, params, rows, parity):
+def torch_cpu_baseline(pipe, H, W, params, cpu, parity):
     """The reference's CPU render path timed on this host's cores: the torch-CPU
     restatement of _render_pytorch (oracle/torch_render.py: torch's own CPU
-    kernels, MKL GEMMs) on a bounded strip of test view 0, with its agreement
-    with the GPU on the same strip."""
+    kernels, MKL GEMMs) on a bounded strip of test view 0 (sized to ~10-30 s on
+    the threads used), with its agreement with the GPU on the same strip."""
     sys.path.insert(0, REPO)
     from oracle import torch_render as TR
     import torch
+    rows = int(min(200, max(48, 3 * cpu["threads_used"])))
     pose, K = lego_camera(H, W, 0)
     r0, sl = _strip(H, W, rows)
     ro, rd = TR.camera_rays(H, W, pose, K)
@@ -502,12 +554,161 @@ def torch_cpu_baseline(pipe, H, W, params, rows, parity):
     g = {k: v.cpu().numpy() for k, v in gpu.items()}
     n = rows * W
     return {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(torch.get_num_threads()),
-            "kind": "port", "seconds": t_cpu, "host_cpus": os.cpu_count(),
-            "cpu_model": _cpu_model(),
+            "kind": "port", "seconds": t_cpu, "host": cpu,
             "sample": f"rows {r0}-{r0 + rows - 1} of lego test view 0 at {H}x{W} ({n} rays, "
                       f"64c+128f) rendered by oracle/torch_render.py (torch-CPU restatement of "
-                      f"_render_pytorch, {torch.get_num_threads()} threads)",
+                      f"_render_pytorch) on {torch.get_num_threads()} threads",
             "agreement_with_gpu": {k: v for k, v in _parity(g, ref, n).items()}}
+
+
+def torch_cpu_baseline_c1(params, cpu, dev):
+    """BASELINE configs[0] / SURVEY §8d "C1 is timed fully": lego 400x400, 64
+    coarse samples, no fine pass, ESS/ERT off -- the whole frame through the
+    torch-CPU restatement on the host's cores (the reference's run.py:36-42
+    times render(batch) the same way: wall clock around one frame), next to the
+    HIP pipeline's time for the same frame."""
+    sys.path.insert(0, REPO)
+    from oracle import torch_render as TR
+    import torch
+    from nerfhip.render import NerfPipeline
+    H = W = 400
+    pose, K = lego_camera(H, W, 0)
+    ro, rd = TR.camera_rays(H, W, pose, K)
+    t0 = time.perf_counter()
+    ref = TR.render_rays(ro, rd, params, N_importance=0)
+    t_cpu = time.perf_counter() - t0
+    pipe = NerfPipeline(dev, N_samples=64, N_importance=0)
+    pipe.set_weights(params)
+    pipe.render_image(H, W, pose, K)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        g = pipe.render_image(H, W, pose, K)
+    torch.cuda.synchronize()
+    t_gpu = (time.perf_counter() - t0) / 5
+    e = float(np.abs(g["rgb_map_0"].cpu().numpy() - ref["rgb_map_0"].numpy().reshape(-1, 3)).max())
+    return {"value": H * W / t_cpu / 1e6, "unit": "Mrays/s", "seconds_per_frame": t_cpu,
+            "cores": int(torch.get_num_threads()), "kind": "port",
+            "sample": f"one whole lego test view 0 at {H}x{W}, 64 coarse samples, N_importance 0 "
+                      f"(oracle/torch_render.py on {torch.get_num_threads()} threads)",
+            "hip_ms_per_frame": t_gpu * 1e3, "hip_Mrays_s": H * W / t_gpu / 1e6,
+            "max_abs_err_rgb_map_0_hip_vs_cpu": e}
+
+
+def host_cpus():
+    """This host's CPUs as the process sees them: logical CPUs, the affinity
+    set, a cgroup CPU quota, physical cores and sockets (/proc/cpuinfo). The
+    CPU baseline runs on threads_used = min(physical cores, affinity, quota)."""
+    logical = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = logical
+    quota = None
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(f) as fh:
+                q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    cores, sockets, phys = set(), set(), None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                    sockets.add(phys)
+                elif line.startswith("core id"):
+                    cores.add((phys, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    physical = len(cores) or logical
+    use = min(physical, aff, max(1, int(quota)) if quota else aff)
+    return {"cpu_model": _cpu_model(), "logical_cpus": logical, "sockets": len(sockets) or None,
+            "physical_cores": physical, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "threads_used": max(1, use)}
+
+
+def ert_report(pipe, rays, world, segment, dev):
+    """C4: MLP samples evaluated per ray with the ERT compaction, and how much of
+    the frame the reference's termination rule touches (summed over ranks)."""
+    import torch
+    import torch.distributed as dist
+    term = pipe.ert_termination()
+    ev, full = pipe.evaluated_samples()
+    v = [ev, full]
+    for S in (64, 192):
+        v += term.get(S, [0, 0, 0, 0])
+    if world > 1:
+        t = torch.tensor(v, device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        v = [int(x) for x in t.tolist()]
+    ev, full = v[0], v[1]
+    out = {"evaluated_samples_per_ray": ev / rays, "full_samples_per_ray": full / rays,
+           "evaluated_fraction": ev / max(1, full),
+           "note": "MLP samples evaluated per ray (coarse 64 + fine 192 in full) with depth "
+                   f"segments of {segment} and rays retired at T < 0.01 (their later weights are "
+                   "zeroed by _raw2outputs_with_ert, VR:1115-1123)"}
+    for i, (S, kind) in enumerate(((64, "coarse"), (192, "fine"))):
+        n, ret, nch, chr_ = v[2 + 4 * i: 6 + 4 * i]
+        out[kind] = {"rays_retired_frac": ret / max(1, n),
+                     "chunks_with_retired_ray_frac": chr_ / max(1, nch), "chunks": nch}
+    return out
+
+
+def reference_frame_parity(pipe, name, H, W, ckpt):
+    """The whole frame against the reference's OWN render of it
+    (tests/golden/<name>.npz, tests/golden/make_ref_frames.py: the reference's
+    Renderer on the CPU with the same checkpoint): map errors, fine-rgb pixels
+    within 1e-5, PSNR of each against the frame's ground truth (evaluators/
+    nerf.py:465-473) and their difference (north_star: within 0.01 dB); for C4
+    also the final occupancy grid and call counter."""
+    import hashlib
+    import torch
+    from nerfhip.evaluate import composite_white, decode_png, psnr
+    from nerfhip.checkpoint import resolve
+    path = os.path.join(REPO, "tests", "golden", name + ".npz")
+    if not os.path.exists(path) or H != 800 or W != 800:
+        return {"skipped": "no reference frame for this size"}
+    z = np.load(path)
+    if ckpt is None or "ckpt_sha256" not in z:
+        return {"skipped": "synthetic weights: the reference frames use the lego checkpoint"}
+    with open(resolve(ckpt), "rb") as f:
+        if hashlib.sha256(f.read()).hexdigest() != str(z["ckpt_sha256"]):
+            return {"skipped": "checkpoint differs from the one the reference frame used"}
+    if bool(z["ess"]):
+        from nerfhip.synthetic import make_occupancy_grid
+        gs = z["grid_spec"]
+        pipe.set_grid(make_occupancy_grid(int(gs[0]), int(gs[1]), float(gs[2]), float(gs[3])))
+        pipe.grid_update_counter = int(z["counter0"])
+    pipe.ert_stats = []
+    g = {k: v.cpu().numpy() for k, v in pipe.render_image(H, W, z["pose"], z["K"]).items()}
+    torch.cuda.synchronize()
+    n = H * W
+    gt = composite_white(decode_png(z["gt_png"]))
+    ref_rgb = z["out_rgb_map"]
+    e = np.abs(g["rgb_map"].reshape(n, 3).astype(np.float64) - ref_rgb.reshape(n, 3)).max(-1)
+    mse = float(np.mean((g["rgb_map"].reshape(n, 3).astype(np.float64) - ref_rgb.reshape(n, 3)) ** 2))
+    p_hip, p_ref = psnr(g["rgb_map"].reshape(H, W, 3), gt), psnr(ref_rgb, gt)
+    out = {"frame": f"lego test view {int(z['frame'])}", "fixture": f"tests/golden/{name}.npz",
+           "max_abs_err_rgb_map_0": float(np.abs(g["rgb_map_0"].reshape(n, 3)
+                                                 - z["out_rgb_map_0"].reshape(n, 3)).max()),
+           "max_abs_err_acc_map_0": float(np.abs(g["acc_map_0"].reshape(n)
+                                                 - z["out_acc_map_0"].reshape(n)).max()),
+           "max_abs_err_rgb_map": float(e.max()),
+           "fine_rgb_pixels_within_1e-5": float(np.mean(e <= 1e-5)),
+           "psnr_hip_vs_reference": float("inf") if mse == 0 else -10 * np.log10(mse),
+           "psnr_vs_gt_hip": p_hip, "psnr_vs_gt_reference": p_ref, "dpsnr_db": p_hip - p_ref,
+           "reference_cpu_seconds": float(z["cpu_seconds"]),
+           "reference_torch_threads": int(z["torch_threads"])}
+    if bool(z["ess"]):
+        out["grid_final_equal"] = bool(np.array_equal(
+            np.packbits(pipe.grid.cpu().numpy().astype(bool)), z["grid_final_bits"]))
+        out["counter_final_equal"] = pipe.grid_update_counter == int(z["grid_counter_final"])
+        pipe.evaluated_samples()
+    return out
 
 
 def _cpu_model():
@@ -521,22 +722,27 @@ def _cpu_model():
     return None
 
 
-def psnr_vs_gt(pipe, H, W, parity):
-    """North_star "PSNR within 0.01 dB on lego": the evaluator's PSNR / SSIM
+def testset_eval(frame, H, W, rank, parity):
+    """North_star "PSNR on lego" over the test set: the evaluator's PSNR / SSIM
     (evaluators/nerf.py:465-504; nerfhip.evaluate) of the HIP render of every
-    packed lego test view (data/lego/test.npz: frames 0, 8, ..., 192) against its
-    ground truth, and on the parity strip the same PSNR for the HIP render and
-    for the oracle's render of those rays (|dPSNR| is the north_star figure)."""
+    packed lego test view (data/lego/test.npz: frames 0, 8, ..., 192, rendered at
+    their packed poses, sharded over the ranks like the timed frames) against
+    its ground truth, on rank 0; and on the parity strip the same PSNR for the
+    HIP render and for the oracle's render of those rays."""
     import torch
     from nerfhip.evaluate import load_packed, psnr, ssim
-    gts, _, _, frames = load_packed(GT_PATH, H, W)
+    gts, poses, focal, frames = load_packed(GT_PATH, H, W)
+    K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
     vals, ssims = [], []
     for i, fr in enumerate(frames):
-        pose, K = lego_camera(H, W, i)
-        rgb = pipe.render_image(H, W, pose, K)["rgb_map"].view(H, W, 3).cpu().numpy()
-        vals.append(psnr(rgb, gts[i]))
-        ssims.append(ssim(rgb, gts[i]))
+        rgb = frame(poses[i], K)["rgb_map"]
+        if rank == 0:
+            rgb = rgb.reshape(H, W, 3).cpu().numpy()
+            vals.append(psnr(rgb, gts[i]))
+            ssims.append(ssim(rgb, gts[i]))
     torch.cuda.synchronize()
+    if rank != 0:
+        return None
     out = {"frames": [int(f) for f in frames], "psnr": vals, "psnr_mean": float(np.mean(vals)),
            "ssim_mean": float(np.mean(ssims)),
            "metric": "evaluators/nerf.py PSNR (clip to [0,1], -10 log10 mse) and SSIM, "
@@ -544,6 +750,7 @@ def psnr_vs_gt(pipe, H, W, parity):
     if parity and "_maps" in parity:
         g, o = parity.pop("_maps")
         r0, r1 = parity["strip_rows"]
+        assert int(frames[0]) == 0
         gt = gts[0][r0:r1]
         pg, po = psnr(g, gt), psnr(o, gt)
         out["strip"] = {"rows": [r0, r1], "frame": int(frames[0]), "psnr_hip": pg,
@@ -551,34 +758,45 @@ def psnr_vs_gt(pipe, H, W, parity):
     return out
 
 
-def cpu_baseline_c4(pipe, H, W, params, rows):
-    """ESS + ERT: the oracle on the frame's first whole 2048-ray chunks (about
-    `rows` rows), fresh grid and call counter on both sides."""
+def cpu_baseline_c4(pipe, H, W, params, rows, cpu):
+    """ESS + ERT: the parity oracle (oracle/nerf_oracle.py) on whole 2048-ray
+    chunks across the middle of test view 0 (through the object: ERT
+    terminations and the chunk-wide argmax rule, VR:1115-1123), after replaying
+    chunk 0 -- whose coarse ERT call updates the occupancy grid at counter 0
+    (VR:1147-1155) -- on both sides, so the window sees the updated grid; each
+    window chunk at its own call counter. Timed: the window on the CPU."""
     sys.path.insert(0, REPO)
     from oracle import nerf_oracle as O
     from nerfhip.synthetic import make_occupancy_grid
     import torch
-    threads = _threads()
     pose, K = lego_camera(H, W, 0)
-    n = max(1, rows * W // 2048) * 2048
+    nch = max(1, rows * W // 2048)
+    c0 = (H * W // 2) // 2048 - nch // 2
+    a, b = c0 * 2048, (c0 + nch) * 2048
     ro, rd = O.camera_rays(H, W, pose, K)
     grid = make_occupancy_grid(0, 128, 1.2, 0.1)
     cfg = O.RenderConfig(N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
                          ert_threshold=0.01)
+    O.render(1, 2048, pose, K, params, cfg, grid=grid, grid_counter=0,
+             rays=(ro[:2048], rd[:2048]))                   # chunk 0: the grid update
     t0 = time.perf_counter()
-    ref, _ = O.render(1, n, pose, K, params, cfg, grid=grid.copy(), grid_counter=0,
-                      rays=(ro[:n], rd[:n]))
+    ref, _ = O.render(1, b - a, pose, K, params, cfg, grid=grid, grid_counter=2 * c0,
+                      rays=(ro[a:b], rd[a:b]))
     t_cpu = time.perf_counter() - t0
     pipe.grid_update_counter = 0
-    gpu = pipe.render_image(H, W, pose, K, p0=0, n=n)
+    gpu = pipe.render_chunks(H, W, pose, K, list(range(c0, c0 + nch)))
     torch.cuda.synchronize()
     g = {k: v.cpu().numpy() for k, v in gpu.items()}
+    n = b - a
     parity = _parity(g, ref, n)
-    parity["rays"] = [0, n]
-    base = {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(threads), "kind": "port",
-            "seconds": t_cpu,
-            "sample": f"rays 0-{n - 1} ({n // 2048} whole 2048-ray chunks) of lego test frame 0 "
-                      f"at {H}x{W}, 64c+128f, ESS + ERT, rendered by oracle/nerf_oracle.py"}
+    parity["rays"] = [a, b]
+    parity["chunks"] = [c0, c0 + nch]
+    parity["acc_map_mean_ref"] = float(np.nanmean(ref["acc_map"]))
+    base = {"value": n / t_cpu / 1e6, "unit": "Mrays/s", "cores": int(_threads()),
+            "kind": "port", "seconds": t_cpu, "host": cpu,
+            "sample": f"rays {a}-{b - 1} ({nch} whole 2048-ray chunks through the object, after "
+                      f"chunk 0's grid update) of lego test view 0 at {H}x{W}, 64c+128f, ESS + "
+                      f"ERT, rendered by oracle/nerf_oracle.py (numpy)"}
     return base, parity
 
 

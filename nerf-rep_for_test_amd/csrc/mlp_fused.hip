@@ -165,13 +165,9 @@ __device__ __forceinline__ void encode(const float (&p)[3], int g4, f32x4 (&out)
       const int f = pa / 3, c = pa - 3 * (pa / 3);
       const float x = c == 0 ? p[0] : (c == 1 ? p[1] : p[2]);
       const float arg = x * (float)(1 << f);    // 2^f exact: x * 2^f is exact
-#if defined(ABL_NOENC)
-      v = arg;
-#else
       float sv, cv;
       sincosf(arg, &sv, &cv);
       v = (g4 & 1) ? cv : sv;
-#endif
     }
     out[(1 + t) >> 2][(1 + t) & 3] = v;
   }
@@ -184,13 +180,8 @@ __device__ __forceinline__ void bias_act(f32x4 (&act)[T], const f32x4 (&acc)[T],
   for (int m = 0; m < T; ++m) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-#if defined(ABL_NOEPI)
-      act[m][r] = acc[m][r];
-      (void)bias; (void)relu;
-#else
       const float v = acc[m][r] + bias[4 * m + r];
       act[m][r] = relu ? fmaxf(v, 0.0f) : v;
-#endif
     }
   }
 }

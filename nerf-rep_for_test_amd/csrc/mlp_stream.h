@@ -28,9 +28,6 @@ constexpr int kHeadRgbW = 2692;       // [3][4][32]
 constexpr int kHeadRgbB = 3076;       // [3]
 constexpr int kHeadScales = 3080;     // mlp_x3: per-layer weight scale exponents [10]
 
-// Ablation switches for timing-only builds (tools/mlp_ablate.py); the shipped
-// library defines none of them. ABL_NOBAR drops the per-slice barriers,
-// ABL_NODMA the weight staging, ABL_NOENC the sin/cos, ABL_NOEPI the bias/ReLU.
 // One 1-KiB LDS-DMA piece (of the 4 each wave stages per slice): block
 // wave*4 + j of slice `src` into the same block of LDS buffer `dst`.
 // The piece index J is the instruction's immediate offset, which applies to the
@@ -39,10 +36,12 @@ constexpr int kHeadScales = 3080;     // mlp_x3: per-layer weight scale exponent
 // DMA of one future slice by one wave, spread over the MFMA groups of the
 // current one: this lane's source (block wave*4 of the slice) and the wave's
 // LDS destination; live is false when there is no slice left to stage.
-// MLP_DMA_BUF: the pieces as `buffer_load_dwordx4 ... lds` against one buffer
-// descriptor of the packed network: the slice's byte offset rides in an SGPR
-// (soffset) and each lane's 32-bit offset in the wave's 4 blocks is constant
-// for the whole kernel, instead of a 64-bit per-lane address per slice.
+// MLP_DMA_BUF (set by the including kernel file, not a tuning switch: the x3
+// kernel defines 1, the FP32 kernel leaves 0): the pieces as `buffer_load_dwordx4
+// ... lds` against one buffer descriptor of the packed network -- the slice's
+// byte offset rides in an SGPR (soffset) and each lane's 32-bit offset in the
+// wave's 4 blocks is constant for the whole kernel -- instead of
+// global_load_lds with a 64-bit per-lane address per slice.
 #ifndef MLP_DMA_BUF
 #define MLP_DMA_BUF 0
 #endif
@@ -79,9 +78,6 @@ __device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf,
 // pieces 0-3; pieces 4-7 move the LDS base and soffset by 4 KiB
 template <int J>
 __device__ __forceinline__ void stage_piece(const Dma& d) {
-#if defined(ABL_NODMA)
-  return;
-#endif
   __builtin_amdgcn_raw_ptr_buffer_load_lds(d.rsrc, (lds_ptr_t)(d.dst + (J / 4) * 1024), 16,
                                            d.voff, d.soff + (J / 4) * 4096, (J % 4) * 1024, 0);
 }
@@ -104,9 +100,6 @@ __device__ __forceinline__ Dma make_dma(const float4* slices, int t, float* buf,
 
 template <int J>
 __device__ __forceinline__ void stage_piece(const Dma& d) {
-#if defined(ABL_NODMA)
-  return;
-#endif
   __builtin_amdgcn_global_load_lds((const void*)d.src, (lds_ptr_t)d.dst, 16, J * 1024, 0);
 }
 #endif
@@ -161,24 +154,18 @@ struct Ring {
 // PENDING slices (of PIECES pieces each per wave) allowed to stay in flight
 template <int PENDING, int PIECES = 4>
 __device__ __forceinline__ void slice_end() {
-#if !defined(ABL_NOBAR)
   constexpr int n = (PENDING >= 2 ? 2 : PENDING) * PIECES;
   static_assert(n < 64, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(n) : "memory");
   __builtin_amdgcn_s_barrier();
-#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 
 // Cross-lane exchange of the 4 lane groups (rows of 16 lanes) that hold one
-// sample. MLP_PERMLANE: gfx950's v_permlane16_swap / v_permlane32_swap (VALU,
-// no LDS traffic or lgkmcnt wait): swapping a value with itself leaves the
+// sample: gfx950's v_permlane16_swap / v_permlane32_swap (VALU, no LDS traffic
+// or lgkmcnt wait, unlike ds_bpermute): swapping a value with itself leaves the
 // row pair (r0, r1) as (r0, r0) | (r1, r1), so a lane sees its xor-16 (xor-32)
-// partner in the other result. Otherwise ds_bpermute through __shfl_xor.
-#ifndef MLP_PERMLANE
-#define MLP_PERMLANE 1
-#endif
-#if MLP_PERMLANE
+// partner in the other result.
 // (v[l], v[l ^ 16]) in some order: both results of the swap
 __device__ __forceinline__ void pair16(float v, float& a, float& b) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -190,22 +177,16 @@ __device__ __forceinline__ void pair32(float v, float& a, float& b) {
   a = __uint_as_float(r[0]);
   b = __uint_as_float(r[1]);
 }
-#endif
 
 // sum over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48);
 // every lane of the quad ends with the bitwise-same value
-// ((v_l + v_l^16) + (v_l^32 + v_l^48) on either path: addition commutes)
+// ((v_l + v_l^16) + (v_l^32 + v_l^48): addition commutes)
 __device__ __forceinline__ float quad_sum(float v) {
-#if MLP_PERMLANE
   float a, b;
   pair16(v, a, b);
   v = a + b;
   pair32(v, a, b);
   return a + b;
-#else
-  v = v + __shfl_xor(v, 16);
-  return v + __shfl_xor(v, 32);
-#endif
 }
 
 }  // namespace nerfhip

@@ -26,10 +26,8 @@
 // g = l>>4, slots j = 0..7 = rows 16(2q + (j>>2)) + 4g + (j&3), i.e. registers
 // r of tiles 2q and 2q+1 (nerfhip/pack.py packs W with that K permutation).
 // this kernel's weight stream: buffer-form LDS-DMA (mlp_stream.h), issued by
-// waves 0-3 only (MLP_X3_LOADERS below)
-#ifndef MLP_DMA_BUF
+// waves 0-3 only (x3_dma below)
 #define MLP_DMA_BUF 1
-#endif
 #include "x3_ops.h"
 
 namespace nerfhip {
@@ -41,79 +39,30 @@ constexpr int kX3Slices = NERF_MLP_X3_SLICES;
 constexpr int kX3Threads = 64 * kStreamWaves;
 constexpr int kX3Tile = 16 * kStreamWaves;
 
-#ifndef MLP_X3_STAGGER
-#define MLP_X3_STAGGER 0
-#endif
-#ifndef MLP_X3_ILV   // >0: interleave the hook's VALU into the group's MFMAs (per gap)
-#define MLP_X3_ILV 2
-#endif
-
-
 // Cross-slice fragment prefetch: the last group of a slice issues the reads of
 // the NEXT slice's group 0 (register set x), so a slice starts its MFMAs right
 // after the barrier instead of exposing one LDS latency per slice. The next
 // slice must then be visible one barrier earlier: x3_slice_end certifies slice
 // g+2 at the end of slice g.
-#ifndef MLP_X3_XPF
-#define MLP_X3_XPF 1
-#endif
 
 // The fragment register sets, live across slices (x: even groups, y: odd).
 struct FragPipe {
   Frags x, y;
-  int late;   // wave-uniform: this wave runs half a slice behind (MLP_X3_HALF)
 };
 
-// Half-slice stagger (MI355X_MICROARCH "Two waves per SIMD", item 9): waves 4-7
-// (the SIMD partners of waves 0-3) pass each slice's barrier after its group 3
-// instead of after group 7, so partners run half a slice apart and their VALU
-// bursts (epilogue, splits) land beside the other's MFMAs. Needs the weight
-// DMA two slices ahead (a late wave still reads slice g-1 after barrier g-1)
-// and every barrier to certify the wave's own pieces (vmcnt(0)).
-#ifndef MLP_X3_HALF
-#define MLP_X3_HALF 0
-#endif
-constexpr int kX3DmaAhead = MLP_X3_HALF ? 2 : 3;
+// The weight stream runs three slices ahead of the compute.
+constexpr int kX3DmaAhead = 3;
+constexpr int kX3Pieces = 8;   // LDS-DMA pieces per loading wave and slice
 
-// MLP_X3_LOADERS=4: only waves 0-3 stage weights (8 pieces each, buffer form),
-// so a loading wave's SIMD partner keeps issuing MFMAs meanwhile.
-#ifndef MLP_X3_LOADERS
-#define MLP_X3_LOADERS 4
-#endif
-// MLP_X3_PERSIST: one workgroup per CU loops over sample tiles; the weight
-// stream continues from one tile's last slice into the next tile's first, so
-// a tile starts on slices already resident instead of a staged prologue.
-#ifndef MLP_X3_PERSIST
-#define MLP_X3_PERSIST 1
-#endif
-#ifndef MLP_X3_LOADER_SPLIT
-#define MLP_X3_LOADER_SPLIT 0
-#endif
-constexpr int kX3Pieces = MLP_X3_LOADERS == 4 ? 8 : 4;   // per loading wave and slice
-// MLP_X3_LOADER_HI: the loading half is waves 4-7 (the second-dispatched half)
-#ifndef MLP_X3_LOADER_HI
-#define MLP_X3_LOADER_HI 0
-#endif
-// MLP_X3_PRIO: s_setprio 1 for waves 4-7 (1) or for waves 0-3 (2) before the
-// tile loop (MI355X_MICROARCH "Two waves per SIMD", item 4)
-#ifndef MLP_X3_PRIO
-#define MLP_X3_PRIO 0
-#endif
+// Only waves 0-3 stage weights (8 pieces each, buffer form), so a loading
+// wave's SIMD partner (waves 4-7) keeps issuing MFMAs meanwhile (+1.6 %).
+// The kernel is persistent (one workgroup per CU loops over sample tiles) and
+// the weight stream continues from one tile's last slice into the next tile's
+// first, so a tile starts on slices already resident instead of a staged
+// prologue. Measured and dropped (round 2): a half-slice stagger of the SIMD
+// partners, other loader splits and wave priorities, workgroup start skews.
 __device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane) {
-#if MLP_X3_LOADERS == 4
-  static_assert(MLP_DMA_BUF, "4 loader waves need the buffer-form DMA");
-  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane,
-                         MLP_X3_LOADER_HI ? wave >= 4 : wave < 4, kX3Slices);
-#else
-  static_assert(MLP_DMA_BUF, "the x3 stream (kX3Slices) needs the buffer-form DMA");
-  return make_dma_blocks(slices, t, buf, wave * kBlocksPerWave, wave, lane, true, kX3Slices);
-#endif
-}
-
-__device__ __forceinline__ void x3_barrier_now() {
-#if MLP_X3_HALF
-  slice_end<0>();
-#endif
+  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4, kX3Slices);
 }
 
 // Group G of NG: drain its fragment reads (issued one group earlier), issue
@@ -131,7 +80,7 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, unsigned nba
     if constexpr (G + 1 < NG) {
       if constexpr ((G & 1) == 0) load_frags<G + 1>(y, base);
       else load_frags<G + 1>(x, base);
-    } else if constexpr (NEXT && MLP_X3_XPF) {
+    } else if constexpr (NEXT) {
       static_assert((G & 1) == 1, "the last group computes from set y");
       load_frags<0>(x, nbase);
     }
@@ -140,95 +89,48 @@ __device__ __forceinline__ void run_group3(Acc& acc, unsigned base, unsigned nba
     constexpr int m = Cfg::tile(G);
     if constexpr ((G & 1) == 0) mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], x, bv[Cfg::bsel(G)]);
     else mfma3x2<Cfg::first(G)>(acc[m], acc[m + 1], y, bv[Cfg::bsel(G)]);
-#if MLP_X3_ILV
-    // the hook's VALU in the gaps of this group's own MFMAs: MFMA, k VALU, ...
+    // the hook's VALU in the gaps of this group's own MFMAs: MFMA, 2 VALU, ...
     hook.template after<G>(acc);
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, MLP_X3_ILV, 0); // up to k VALU
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // up to 2 VALU
     }
-#endif
     __builtin_amdgcn_sched_barrier(0);
-#if MLP_X3_LOADERS == 4
-    // waves 0-3 stage 8 pieces each, their partners none
+    // waves 0-3 stage 8 pieces each (after group 0), their partners none
     if constexpr (G == 0) {
       if (dma.live) {
         stage_piece<0>(dma); stage_piece<1>(dma); stage_piece<2>(dma); stage_piece<3>(dma);
-#if !MLP_X3_LOADER_SPLIT
-        stage_piece<4>(dma); stage_piece<5>(dma); stage_piece<6>(dma); stage_piece<7>(dma);
-#endif
-      }
-    }
-#if MLP_X3_LOADER_SPLIT
-    if constexpr (G == MLP_X3_LOADER_SPLIT) {
-      if (dma.live) {
         stage_piece<4>(dma); stage_piece<5>(dma); stage_piece<6>(dma); stage_piece<7>(dma);
       }
     }
-#endif
-#elif !defined(MLP_X3_SPREAD_DMA)
-    // the wave's 4 pieces back to back after group 0 (one address/M0 setup;
-    // measured +2.4 % over one piece every other group)
-    if constexpr (G == 0) {
-      if (dma.live) {
-        stage_piece<0>(dma); stage_piece<1>(dma); stage_piece<2>(dma); stage_piece<3>(dma);
-      }
-    }
-#elif MLP_X3_STAGGER
-    if constexpr (G / 2 < kBlocksPerWave) {
-      if (dma.live && (G & 1) == (dma.wave >> 2)) stage_piece<G / 2>(dma);
-    }
-#else
-    if constexpr ((G & 1) == 0 && G / 2 < kBlocksPerWave) {
-      if (dma.live) stage_piece<G / 2>(dma);
-    }
-#endif
-#if !MLP_X3_ILV
-    hook.template after<G>(acc);
-#endif
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (MLP_X3_HALF && G == 3 && NG == 8) {
-      if (fp.late) x3_barrier_now();
-    }
     run_group3<G + 1, NG, Cfg, NEXT>(acc, base, nbase, bv, fp, dma, hook);
   }
 }
 
-// Slice g of the stream (NG groups). With MLP_X3_XPF its group 0 fragments were
-// issued by the previous slice's last group (or the kernel prologue).
+// Slice g of the stream (NG groups). Its group 0 fragments were issued by the
+// previous slice's last group (or the kernel prologue).
 template <int NG, typename Cfg, bool NEXT = true, typename Acc, typename BV, typename Hook>
 __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const BV& bv,
                                            FragPipe& fp, Hook& hook) {
   const unsigned base = lds_base(R.buf(g), R.lane);
-#if !MLP_X3_XPF
-  load_frags<0>(fp.x, base);
-#endif
   const int t = g + kX3DmaAhead;
-#if MLP_X3_PERSIST
   // the stream runs on into the next tile (the last tile's wrapped pieces are
   // staged but never read): every slice stages one, every slice_end counts 2
   const int ts = t < kX3Slices ? t : t - kX3Slices;
-#else
-  const int ts = t;
-#endif
   run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp,
                                x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane), hook);
 }
 
-// End of slice g: this wave's LDS-DMA of slice g+2 (XPF; g+1 without) has
-// landed, then one barrier publishes it to every wave and frees slice g's
-// buffer for the DMA issued in slice g+1. INFLIGHT = slices of DMA allowed in
-// flight without the prefetch (2 while the stream has three slices ahead).
+// End of slice g: this wave's LDS-DMA of slice g+2 has landed (the next
+// slice's group 0 fragments are read before this barrier), then one barrier
+// publishes it to every wave and frees slice g's buffer for the DMA issued in
+// slice g+1. INFLIGHT = slices of DMA that could stay in flight without that
+// prefetch (2 while the stream has three slices ahead).
 template <int INFLIGHT>
-__device__ __forceinline__ void x3_slice_end(const FragPipe& fp) {
-#if MLP_X3_HALF
-  if (!fp.late) x3_barrier_now();
-#elif MLP_X3_XPF
+__device__ __forceinline__ void x3_slice_end(const FragPipe&) {
   slice_end<(INFLIGHT > 0 ? INFLIGHT - 1 : 0), kX3Pieces>();
-#else
-  slice_end<INFLIGHT, kX3Pieces>();
-#endif
 }
 
 
@@ -315,13 +217,8 @@ struct EpiHook {
       Op v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-#if defined(ABL_NOEPI)   // timing only; still consumes the prefetched biases
-        v[r] = acc[2 * G][r] + bb[G & 1][0][r];
-        v[4 + r] = acc[2 * G + 1][r] + bb[G & 1][1][r];
-#else
         v[r] = fmaxf(__builtin_fmaf(acc[2 * G][r], inv, bb[G & 1][0][r]), floor);
         v[4 + r] = fmaxf(__builtin_fmaf(acc[2 * G + 1][r], inv, bb[G & 1][1][r]), floor);
-#endif
       }
 #pragma unroll
       for (int j = 0; j < 8; j += 2)
@@ -397,38 +294,20 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   const int wave = tid >> 6;
   Ring R{ring, slices, wave, lane};
 
-#if defined(MLP_X3_SKEW)   // timing experiment: workgroups of one XCD start staggered
-  for (int i = 0; i < (int)((blockIdx.x >> 3) & 7) * MLP_X3_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   for (int t = 0; t < kX3DmaAhead; ++t)
     stage_slice(make_dma(slices, t, R.buf(t), wave, lane));   // all 8 waves, 4 pieces each
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
 
   FragPipe fp;
-  fp.late = MLP_X3_HALF ? __builtin_amdgcn_readfirstlane(wave >> 2) : 0;
-#if MLP_X3_PRIO
-  if (__builtin_amdgcn_readfirstlane(wave >> 2) == (MLP_X3_PRIO == 1 ? 1 : 0))
-    __builtin_amdgcn_s_setprio(1);
-#endif
-#if MLP_X3_PERSIST
   const int64_t ntiles = (total + kX3Tile - 1) / kX3Tile;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const bool first_tile = tile == (int64_t)blockIdx.x;
-#else
-  {
-  const int64_t tile = blockIdx.x;
-  constexpr bool first_tile = true;
-#endif
   const int64_t gs = tile * kX3Tile + wave * 16 + (lane & 15);
-#if MLP_X3_PERSIST
   // recomputed per tile: otherwise the encoding's per-lane constants are
   // hoisted out of the tile loop and, live through every slice, spill
   int g4 = lane >> 4;
   asm volatile("" : "+v"(g4));
-#else
-  const int g4 = lane >> 4;
-#endif
   const bool valid = gs < total;
   const int64_t gl = valid ? gs : total - 1;
   const int64_t gc = LIST ? (int64_t)list[gl] : gl;   // the flat sample index
@@ -448,12 +327,10 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   f32x4 acc[16];   // every layer's first slice starts it from zero
   Op X[8];
   if (first_tile) __syncthreads();   // head, z/rays loads and the three prologue slices resident
-#if MLP_X3_XPF
   // slice 0, group 0 (a later tile's slice 0 was certified by the previous
   // tile's slice 63; not prefetched across tiles: the fragments would stay live
   // through the tail and the encoding)
   load_frags<0>(fp.x, lds_base(R.buf(0), lane));
-#endif
 
   // ---- layer 0: 63 -> 256 (slices 0, 1), epilogue fused into slice 1 --------
   int e = act_exponent(enc_max);
@@ -528,21 +405,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     Split2 h1{{X[4], s}, {X[5], s}};
     run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>(fp);
     Split2 h2{{X[6], s}, {X[7], s}};
-#if MLP_X3_PERSIST
     run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<2>(fp);
     SplitHook h3{dirf, s};
     run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<2>(fp);
     NoHook nh;
     const Op D[1] = {dirf};
     run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh); x3_slice_end<2>(fp);
-#else
-    run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<1>(fp);
-    SplitHook h3{dirf, s};
-    run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<0>(fp);
-    NoHook nh;
-    const Op D[1] = {dirf};
-    run_slice3<4, Step256<0>, false>(acc8, R, g + 4, D, fp, nh);   // the stream's last slice
-#endif
   }
   {   // views epilogue (bias, ReLU) -- once per pass, not pipelined
     const float inv = ldexpf(1.0f, -((int)hd[kHeadScales + 9] + e));
@@ -569,10 +437,8 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   if (valid && g4 == 0) raw[gc] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
   R.rot = (R.rot + kX3Slices) & 3;   // the next tile's slice 0 = this stream's slice 65
   }
-#if MLP_X3_PERSIST
   // the last tile's wrapped DMA pieces land before the workgroup's LDS is freed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 }
 
 
@@ -734,18 +600,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
   // HBM operands as buffer resources: a lane's offset is one 32-bit VGPR, the
   // row offset an SGPR, and a sample past P reads 0 / drops its store (offset
   // pushed past num_records) -- no per-load address registers or branches
-  // X3L_ABL_*: timing-only builds (tools/layer_ablate.sh) whose B loads or C
-  // stores are dropped by a zero-record descriptor; their outputs are wrong
-#if defined(X3L_ABL_NOLOAD)
-  const int nbB = 0;
-#else
   const int nbB = (int)(32 * NK * ldb * 4);
-#endif
-#if defined(X3L_ABL_NOSTORE)
-  const int nbC = 0;
-#else
   const int nbC = (int)(16 * MT * ldc * 4);
-#endif
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, nbC, 0x00020000);
   const int nbM = mask ? (int)(16 * MT * ldm * 4) : 0;
@@ -901,9 +757,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_layer_kernel(
         }
       }
     }
-#if !defined(X3L_ABL_NOWAIT)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile starts clean
-#endif
   }
   if (amax_out) {   // one atomic per workgroup (as ordered uint bits: values >= 0)
     __shared__ unsigned wg_max;
@@ -1343,13 +1197,9 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
   if (total == 0) return 0;
   const int64_t blocks = cdiv(total, kX3Tile);
   NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_forward_x3: too many samples for one launch");
-#if MLP_X3_PERSIST
-  // one workgroup per CU (the ring and head take 140 KiB of the 160 KiB LDS)
+  // persistent: one workgroup per CU (the ring and head take 140 KiB of the 160 KiB LDS)
   const int n_cu = stream_cu_count(stream);
   const int64_t grid = blocks < n_cu ? blocks : n_cu;
-#else
-  const int64_t grid = blocks;
-#endif
   hipLaunchKernelGGL(mlp_x3_kernel<false>, dim3((unsigned)grid), dim3(kX3Threads), 0,
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
                      z_stride, total, S, (float4*)raw, nullptr, nullptr);
@@ -1367,7 +1217,6 @@ extern "C" int nerf_mlp_forward_x3_list(const float* w_slices, const float* w_he
   NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
                    ((uintptr_t)raw & 15) == 0,
                "nerf_mlp_forward_x3_list: weights/raw must be 16-byte aligned");
-  static_assert(MLP_X3_PERSIST, "the list form needs the persistent tile loop");
   if (max_count == 0) return 0;
   const int64_t blocks = cdiv(max_count, kX3Tile);
   NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_forward_x3_list: too many samples");

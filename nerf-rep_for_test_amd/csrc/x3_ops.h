@@ -17,10 +17,6 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 // the FP16 hi halves (VGPRs 0-3) and lo halves (VGPRs 4-7) after it.
 typedef f32x8 Op;
 
-#ifndef MLP_X3_MIXASM   // operand split as 4 hand-placed v_fma_mix per value pair
-#define MLP_X3_MIXASM 1
-#endif
-
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_f16((a), (b), (c), 0, 0, 0)
 
 __device__ __forceinline__ unsigned lds_addr(const float* p) {
@@ -47,91 +43,29 @@ struct Frags {   // one group's A fragments: tiles m, m+1 x (hi, lo)
 
 template <int G>
 __device__ __forceinline__ void load_frags(Frags& f, unsigned base) {
-#if defined(ABL_HALFLDS)   // timing only: half the fragment reads (lo := hi)
-  f.h0 = frag16<4 * G + 0>(base);
-  f.h1 = frag16<4 * G + 2>(base);
-  f.l0 = f.h0;
-  f.l1 = f.h1;
-#else
   f.h0 = frag16<4 * G + 0>(base);
   f.l0 = frag16<4 * G + 1>(base);
   f.h1 = frag16<4 * G + 2>(base);
   f.l1 = frag16<4 * G + 3>(base);
-#endif
 }
 
 // FIRST: the layer's first K step starts the accumulators from zero (no
 // clearing pass over them between layers).
-// MLP_X3_ORD: the order of the 6 products of a tile pair. Shipped: 4, each
-// tile's three products back to back (a dependent accumulator chain), in the
-// same per-tile order as 0 (the previous order, the two tiles interleaved), so
-// the results are bitwise equal; measured 2.7 % faster on the inference kernel
-// (tools/mlp_ablate.py x3_ord*: 23.35 vs 23.99 ms, 160 000 x 64 samples). Every
-// order that keeps a tile's products together (4, 7, 8) runs at that speed;
-// the interleaved ones (0-3, 5) do not (profiles/r2_x3_order.log).
-#ifndef MLP_X3_ORD
-#define MLP_X3_ORD 4
-#endif
+// The order of a tile pair's 6 products: each tile's three back to back (one
+// dependent accumulator chain, the A fragment held for two MFMAs). Measured
+// 2.7 % faster on the inference kernel than the two tiles interleaved (same
+// per-tile summation order, bitwise-equal results; round 2, timing-only A/B:
+// 23.35 vs 23.99 ms over 160 000 x 64 samples, profiles/r2_x3_order.log) --
+// the chip holds a higher clock under the chained order.
 template <bool FIRST>
 __device__ __forceinline__ void mfma3x2(f32x4& c0, f32x4& c1, const Frags& a, const Op& b) {
   const half8 bh = op_hi(b), bl = op_lo(b);
-#if MLP_X3_ORD == 1   // the two small terms first, wh*xh last
-  c0 = MFMA16(a.h0, bl, FIRST ? f32x4(0.0f) : c0);
-  c1 = MFMA16(a.h1, bl, FIRST ? f32x4(0.0f) : c1);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, c1);
-  c0 = MFMA16(a.h0, bh, c0);
-  c1 = MFMA16(a.h1, bh, c1);
-#elif MLP_X3_ORD == 2   // B operand held for 4 MFMAs
-  c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
-  c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, c1);
-  c0 = MFMA16(a.h0, bl, c0);
-  c1 = MFMA16(a.h1, bl, c1);
-#elif MLP_X3_ORD == 3   // A operand held for 2 MFMAs
-  c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
-  c0 = MFMA16(a.h0, bl, c0);
-  c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
-  c1 = MFMA16(a.h1, bl, c1);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, c1);
-#elif MLP_X3_ORD == 4   // one tile's three products, then the other's
   c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
   c0 = MFMA16(a.h0, bl, c0);
   c0 = MFMA16(a.l0, bh, c0);
   c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
   c1 = MFMA16(a.h1, bl, c1);
   c1 = MFMA16(a.l1, bh, c1);
-#elif MLP_X3_ORD == 7   // tile 0's chain, then tile 1's in reverse
-  c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
-  c0 = MFMA16(a.h0, bl, c0);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, FIRST ? f32x4(0.0f) : c1);
-  c1 = MFMA16(a.h1, bh, c1);
-  c1 = MFMA16(a.h1, bl, c1);
-#elif MLP_X3_ORD == 8   // B switched twice per group and not at its boundary
-  c0 = MFMA16(a.h0, bl, FIRST ? f32x4(0.0f) : c0);
-  c0 = MFMA16(a.h0, bh, c0);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, FIRST ? f32x4(0.0f) : c1);
-  c1 = MFMA16(a.h1, bh, c1);
-  c1 = MFMA16(a.h1, bl, c1);
-#elif MLP_X3_ORD == 5   // A held for 2, B switched 3 times
-  c0 = MFMA16(a.h0, bl, FIRST ? f32x4(0.0f) : c0);
-  c0 = MFMA16(a.h0, bh, c0);
-  c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
-  c1 = MFMA16(a.h1, bl, c1);
-  c1 = MFMA16(a.l1, bh, c1);
-  c0 = MFMA16(a.l0, bh, c0);
-#else
-  c0 = MFMA16(a.h0, bh, FIRST ? f32x4(0.0f) : c0);
-  c1 = MFMA16(a.h1, bh, FIRST ? f32x4(0.0f) : c1);
-  c0 = MFMA16(a.h0, bl, c0);
-  c1 = MFMA16(a.h1, bl, c1);
-  c0 = MFMA16(a.l0, bh, c0);
-  c1 = MFMA16(a.l1, bh, c1);
-#endif
 }
 
 // Slice shapes: the tiles, the B operand and whether the group starts its
@@ -157,16 +91,11 @@ struct StepViews {
 // ---------------------------------------------------------------------------
 // max over the 4 lane groups holding one sample (lanes l, l^16, l^32, l^48)
 __device__ __forceinline__ float sample_max(float v) {
-#if MLP_PERMLANE
   float a, b;
   pair16(v, a, b);
   v = fmaxf(a, b);
   pair32(v, a, b);
   return fmaxf(a, b);
-#else
-  v = fmaxf(v, __shfl_xor(v, 16));
-  return fmaxf(v, __shfl_xor(v, 32));
-#endif
 }
 
 // exponent e with max * 2^e in [2^13, 2^14) (0 for an all-zero sample), at
@@ -184,11 +113,6 @@ __device__ __forceinline__ int act_exponent(float mx) {
 
 // FP16 hi/lo of two scaled values, packed: (hi pair, lo pair) as two dwords
 __device__ __forceinline__ void split2(float a, float b, float s, float& hp, float& lp) {
-#if defined(ABL_NOEPI)   // timing only
-  hp = __builtin_bit_cast(float, half2_t{(_Float16)a, (_Float16)b});
-  lp = hp;
-  (void)s;
-#elif MLP_X3_MIXASM
   // hi = f16(a*s), lo = f16(a*s - hi): one mixed-precision fma each (a*s is
   // exact: s is a power of two), written straight into the halves of the packed
   // registers; the residual reads hi's f16 half in place (op_sel). 4 VALU per
@@ -201,16 +125,6 @@ __device__ __forceinline__ void split2(float a, float b, float s, float& hp, flo
       : "+v"(l) : "v"(b), "v"(s), "v"(h));
   hp = h;
   lp = l;
-#else
-  // hi = f16(a*s), lo = f16(a*s - hi): one mixed-precision fma each (a*s is
-  // exact: s is a power of two)
-  const _Float16 ha = (_Float16)(a * s), hb = (_Float16)(b * s);
-  const half2_t h{ha, hb};
-  const half2_t l{(_Float16)__builtin_fmaf(a, s, -(float)ha),
-                  (_Float16)__builtin_fmaf(b, s, -(float)hb)};
-  hp = __builtin_bit_cast(float, h);
-  lp = __builtin_bit_cast(float, l);
-#endif
 }
 
 __device__ __forceinline__ void split_op(Op& v, float s) {
@@ -238,11 +152,7 @@ __device__ __forceinline__ void encode_xyz(const float (&p)[3], int g, Op (&e)[2
       const int f = pr / 3, c = pr - 3 * f;
       const float x = c == 0 ? p[0] : (c == 1 ? p[1] : p[2]);
       const float arg = x * (float)(1 << f);   // exact power of two (freq.py:19)
-#if defined(ABL_NOENC)   // timing only
-      a = arg; b = arg * 0.5f;
-#else
       sincosf(arg, &a, &b);
-#endif
     } else {
       a = t == 6 ? p[0] : (t == 7 ? p[2] : 0.0f);
       b = t == 6 ? p[1] : 0.0f;
@@ -259,11 +169,7 @@ __device__ __forceinline__ void encode_dir(const float (&d)[3], int g, Op& e) {
   for (int t = 0; t < 3; ++t) {
     const float arg = d[t] * (float)(1 << g);
     float sv, cv;
-#if defined(ABL_NOENC)   // timing only
-    sv = arg; cv = arg * 0.5f;
-#else
     sincosf(arg, &sv, &cv);
-#endif
     e[2 * t] = sv;
     e[2 * t + 1] = cv;
   }

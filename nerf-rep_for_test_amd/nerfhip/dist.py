@@ -10,6 +10,14 @@ bands are cut on whole reference chunks instead (``chunk_aligned=True``), and
 with ESS + ERT each rank replays the grid self-updates of the chunks outside
 its band (NerfPipeline.render_band) so that every band sees the grid the
 reference's sequential loop would have at its first chunk.
+
+With ERT's sample compaction a chunk's cost follows the scene (a chunk of
+background retires nothing, one across the object retires most samples), so
+contiguous bands load the ranks unevenly. ``render_frame_interleaved`` deals
+the 2048-ray chunks out round-robin instead (chunk c -> rank
+c mod P; NerfPipeline.render_chunks keeps the reference's sequential grid
+semantics), gathers equal-size padded tiles and puts the chunks back in
+pixel order with one index_select.
 """
 from __future__ import annotations
 
@@ -82,4 +90,49 @@ def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
             q0, qn, _ = band(H, W, r, world, chunk_aligned)
             parts.append(full[r * n_pad:r * n_pad + qn])
         full = torch.cat(parts, 0)
+    return unpack_maps(full, H, W, keys)
+
+
+def chunk_set(H, W, rank, world):
+    """Chunks (2048 consecutive pixels, VR:147) rank `rank` owns under the
+    interleaved assignment c -> c mod world, their pixel count, and the padded
+    tile length (the most chunks any rank owns x 2048)."""
+    total = H * W
+    nch = -(-total // REF_CHUNK)
+    mine = list(range(rank, nch, world))
+    n = sum(min(REF_CHUNK, total - c * REF_CHUNK) for c in mine)
+    return mine, n, -(-nch // world) * REF_CHUNK
+
+
+_PERM = {}
+
+
+def interleave_index(H, W, world, device):
+    """Row of the gathered [world * n_pad] tiles holding each pixel, in pixel order."""
+    key = (H, W, world, str(device))
+    if key not in _PERM:
+        total = H * W
+        _, _, n_pad = chunk_set(H, W, 0, world)
+        pix = torch.arange(total, dtype=torch.int64)
+        c = pix // REF_CHUNK
+        _PERM[key] = ((c % world) * n_pad + (c // world) * REF_CHUNK + pix % REF_CHUNK).to(device)
+    return _PERM[key]
+
+
+def render_frame_interleaved(render_chunks, H, W, rank, world, device, group=None):
+    """render_chunks(chunks) -> dict of flat maps for the concatenated pixels of
+    the given (ascending) chunk ids; called on every rank, also with an empty
+    list, so stateful renderers (ESS + ERT, NerfPipeline.render_chunks) advance
+    their grid and counter everywhere. Returns the assembled frame (dict of
+    [H,W(,3)] maps) on every rank."""
+    mine, n, n_pad = chunk_set(H, W, rank, world)
+    maps = render_chunks(mine) or {}
+    keys = set(maps) if maps else set(MAP_ORDER)
+    tile = pack_maps(maps, n, n_pad, device)
+    if world == 1:
+        full = tile[:H * W]
+    else:
+        full = torch.empty((world * n_pad, 12), device=device, dtype=torch.float32)
+        dist.all_gather_into_tensor(full, tile, group=group)
+        full = full.index_select(0, interleave_index(H, W, world, device))
     return unpack_maps(full, H, W, keys)

@@ -32,6 +32,24 @@ def coarse_depth_table(near, far, n_samples, lindisp):
     return 1. / (1. / near * (1. - t_vals) + 1. / far * t_vals)
 
 
+def reference_draws(n, S, NI, perturb, draw_u, device):
+    """The torch.rand draws the reference's ``_render_pytorch`` makes for n rays, in
+    its order: per 2048-ray chunk (VR:154) the stratification jitter t_rand [m, S]
+    when ``perturb > 0`` (``_sample_coarse`` VR:233-234, or the ESS variant
+    :1080-1085) and then, when ``draw_u`` (``self.net.training``, VR:247-249), the
+    fine-sampling u [m, NI]. Returns (t_rand [n, S] | None, u [n, NI] | None), so
+    a whole-frame pass consumes the same random stream as the chunk loop."""
+    tr, uu = [], []
+    for c0 in range(0, n, REF_CHUNK):
+        m = min(REF_CHUNK, n - c0)
+        if perturb > 0:
+            tr.append(torch.rand((m, S), device=device))
+        if draw_u and NI > 0:
+            uu.append(torch.rand((m, NI), device=device))
+    return (torch.cat(tr).contiguous() if tr else None,
+            torch.cat(uu).contiguous() if uu else None)
+
+
 MLP_KERNELS = {"fp32": ("nerf_mlp_forward", pack_mlp),
                "f16x3": ("nerf_mlp_forward_x3", pack_mlp_x3)}
 
@@ -80,6 +98,10 @@ class NerfPipeline:
         self.fine = None
         self.timer = None         # list -> (start event, end event, samples, bytes) per MLP launch
         self.stage_timer = None   # list -> (kernel, start event, end event, algorithmic bytes)
+        self.capture_zall = None  # list -> the merged fine depths [m, S+NI] of every pass (tests)
+        self._replaying = False   # replays of foreign update chunks: not in ert_stats
+        self._updates_on = True   # render_chunks switches the grid self-update off for blocks
+                                  # of non-consecutive chunks that hold no updating chunk
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, params, coarse_prefix="model", fine_prefix="model_fine"):
@@ -158,7 +180,8 @@ class NerfPipeline:
             if t is not None:
                 e1.record()
                 t.append((e0, e1, cnt, None))
-        self.ert_stats.append((counts, n, S))
+        if not self._replaying:
+            self.ert_stats.append((counts, n, S, active))
         return raw
 
     def _timed(self, name, nbytes, fn):
@@ -245,6 +268,8 @@ class NerfPipeline:
                 self._timed("sample_fine", nb, lambda: call(
                     "nerf_sample_fine", ptr(z), zs, ptr(w), ptr(uu), us, m, S, NI, ptr(zall), st))
                 del raw, w
+                if self.capture_zall is not None:
+                    self.capture_zall.append(zall.clone())
                 raw_f = self._pass_mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
                 w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p,
                                      need_weights=self.enable_ert and self.enable_ess)
@@ -263,11 +288,30 @@ class NerfPipeline:
     def evaluated_samples(self, reset=True):
         """(MLP samples evaluated, samples of a full evaluation) over the ERT
         passes since the last reset (one host sync)."""
-        ev = sum(int(c.sum()) for c, _, _ in self.ert_stats)
-        full = sum(n * S for _, n, S in self.ert_stats)
+        ev = sum(int(c.sum()) for c, _, _, _ in self.ert_stats)
+        full = sum(n * S for _, n, S, _ in self.ert_stats)
         if reset:
             self.ert_stats = []
         return ev, full
+
+    def ert_termination(self):
+        """Per ERT pass kind (samples per ray S: coarse / fine), over the passes
+        since the last reset: rays retired by the sample compaction (transmittance
+        below the threshold before the last depth segment: the reference zeroes
+        their later weights, VR:1115-1123) and reference chunks holding at least
+        one such ray (where the chunk-wide argmax rule applies)."""
+        out = {}
+        for _, n, S, active in self.ert_stats:
+            d = out.setdefault(S, [0, 0, 0, 0])
+            ret = active == 0
+            nch = -(-n // REF_CHUNK)
+            pad = torch.zeros((nch * REF_CHUNK,), device=ret.device, dtype=torch.bool)
+            pad[:n] = ret
+            d[0] += n
+            d[1] += int(ret.sum())
+            d[2] += nch
+            d[3] += int(pad.view(nch, REF_CHUNK).any(1).sum())
+        return out
 
     def _calls_per_chunk(self):
         return 2 if self.N_importance > 0 else 1
@@ -276,7 +320,7 @@ class NerfPipeline:
         """VR:1147-1155: the ERT composite call whose counter is a multiple of the
         interval updates the ESS grid from that chunk's samples (kind 0 = coarse
         call, 1 = fine call of each chunk)."""
-        if not (self.enable_ert and self.enable_ess):
+        if not (self.enable_ert and self.enable_ess and self._updates_on):
             return
         per = self._calls_per_chunk()
         for c in range(-(-m // REF_CHUNK)):
@@ -289,6 +333,8 @@ class NerfPipeline:
     def _ess_phase_len(self, m):
         """Cut a pass after the first chunk that updates the grid, so later
         chunks' ESS sees the updated grid as in the reference's sequential loop."""
+        if not self._updates_on:
+            return m
         per = self._calls_per_chunk()
         c0 = self.grid_update_counter
         for c in range(-(-m // REF_CHUNK)):
@@ -351,7 +397,8 @@ class NerfPipeline:
         def replay(c):
             self.grid_update_counter = cf + per * c
             a = c * REF_CHUNK
-            self.render_image(H, W, pose, K, p0=a, n=min(REF_CHUNK, H * W - a))
+            self._replay(lambda: self.render_image(H, W, pose, K, p0=a,
+                                                   n=min(REF_CHUNK, H * W - a)))
 
         for c in upd:
             if c < c0:
@@ -363,6 +410,91 @@ class NerfPipeline:
                 replay(c)
         self.grid_update_counter = cf + per * total
         return res
+
+    def _replay(self, fn):
+        """Run a replay of a foreign chunk (its grid update only; its samples are
+        not this rank's and stay out of ert_stats)."""
+        self._replaying = True
+        try:
+            return fn()
+        finally:
+            self._replaying = False
+
+    def _update_chunks(self, total):
+        """Chunks of a frame whose ERT calls update the ESS grid (VR:1147-1157),
+        given the counter at the frame's first chunk."""
+        per, cf = self._calls_per_chunk(), self.grid_update_counter
+        return [c for c in range(total)
+                if any((cf + per * c + k) % self.grid_update_interval == 0 for k in range(per))]
+
+    def render_chunks(self, H, W, pose, K, chunks):
+        """The reference chunks `chunks` (ascending ids of 2048 consecutive
+        pixels, VR:147) of a frame whose other chunks other ranks render
+        concurrently (dist.render_frame_interleaved: chunk c on rank c mod P),
+        with the results of the reference's sequential chunk loop. Returns the
+        flat maps of the chunks' pixels, concatenated in the given order
+        ({} for an empty list).
+
+        Without ESS + ERT the chunks render as one block (ERT's chunk rule holds
+        within it: every chunk is whole and keeps its 2048-ray alignment). With
+        both, the ESS grid changes at the chunks whose ERT call counter hits a
+        multiple of grid_update_interval, so the owned chunks are rendered in
+        blocks between those update chunks (grid updates off inside a block,
+        which holds none), each update chunk is rendered -- or, when another
+        rank owns it, replayed and discarded -- at its own counter in chunk
+        order, and the updates after the last owned chunk are replayed too,
+        so every rank leaves the frame with the sequential loop's grid and
+        counter. Cost: one extra chunk per foreign update chunk (2 per 500
+        ERT calls)."""
+        total = -(-H * W // REF_CHUNK)
+        chunks = [int(c) for c in chunks]
+        if chunks != sorted(set(chunks)) or (chunks and not 0 <= chunks[0] <= chunks[-1] < total):
+            raise ValueError("chunks must be ascending, distinct ids of the frame's chunks")
+        per, cf = self._calls_per_chunk(), self.grid_update_counter
+        rays_o, rays_d = self.camera_rays(H, W, pose, K)
+        lens = [min(REF_CHUNK, H * W - c * REF_CHUNK) for c in chunks]
+        offs = [0]
+        for ln in lens:
+            offs.append(offs[-1] + ln)
+        outputs = self.alloc_outputs(offs[-1]) if chunks else None
+
+        def rows(cs):
+            idx = torch.cat([torch.arange(c * REF_CHUNK, c * REF_CHUNK + min(
+                REF_CHUNK, H * W - c * REF_CHUNK), device=self.device) for c in cs])
+            return rays_o.index_select(0, idx), rays_d.index_select(0, idx)
+
+        def block(i0, i1):           # own chunks chunks[i0:i1] as one block, no updates inside
+            if i1 <= i0:
+                return
+            ro, rd = rows(chunks[i0:i1])
+            self._updates_on = False
+            try:
+                self.render_rays(ro, rd, outputs=outputs, off=offs[i0])
+            finally:
+                self._updates_on = True
+
+        if not (self.enable_ess and self.enable_ert):
+            block(0, len(chunks))
+            if self.enable_ert:
+                self.grid_update_counter = cf + per * total
+            return maps_dict(outputs) if chunks else {}
+        i = 0
+        for u in self._update_chunks(total):
+            j = i
+            while j < len(chunks) and chunks[j] < u:
+                j += 1
+            block(i, j)
+            i = j
+            self.grid_update_counter = cf + per * u
+            ro, rd = rows([u])
+            if i < len(chunks) and chunks[i] == u:
+                self.render_rays(ro, rd, outputs=outputs, off=offs[i])
+                i += 1
+            else:
+                self._replay(lambda: self.render_rays(ro, rd))
+        block(i, len(chunks))
+        self.grid_update_counter = cf + per * total
+        return maps_dict(outputs) if chunks else {}
 
     def render_image(self, H, W, pose, K, t_rand=None, u=None, p0=0, n=None):
         """Render pixels [p0, p0+n) of an H x W image; returns the reference's map dict

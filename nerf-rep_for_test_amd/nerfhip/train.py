@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import call, ptr
-from .render import REF_CHUNK, coarse_depth_table
+from .render import REF_CHUNK, coarse_depth_table, reference_draws
 
 XYZ_FREQS, DIR_FREQS = 10, 4
 
@@ -187,15 +187,7 @@ def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
         if pipe.enable_ess and pipe.enable_ert:
             m = pipe._ess_phase_len(m)
         ro, rd = rays_o[p:p + m], rays_d[p:p + m]
-        tr, uu = [], []
-        for c0 in range(0, m, REF_CHUNK):
-            mc = min(REF_CHUNK, m - c0)
-            if perturb > 0:
-                tr.append(torch.rand((mc, S), device=dev))
-            if NI > 0:
-                uu.append(torch.rand((mc, NI), device=dev))
-        t_rand = torch.cat(tr).contiguous() if tr else None
-        u = torch.cat(uu).contiguous() if uu else None
+        t_rand, u = reference_draws(m, S, NI, perturb, True, dev)
         z = torch.empty((m, S), device=dev, dtype=torch.float32)
         if pipe.enable_ess:
             if pipe.grid is None:
@@ -328,41 +320,49 @@ class NerfTrainer:
         """One optimisation step; returns the loss dict (device tensors). With a
         process group, each rank's gradients are averaged (data parallel: one
         flat bucket, one all-reduce over RCCL) before clipping and Adam.
-        In graph mode (no explicit draws given) the first two steps of a batch
-        shape run eagerly (they create the packers' buffers, Adam's state and
-        the BLAS handles), the third is captured and every step from then on
-        replays the graph with the batch copied into its static inputs; the
-        returned losses are the graph's output tensors."""
-        if self.graph and t_rand is None and u is None:
-            return self._step_graphed(rays_o, rays_d, target, group)
+        ``t_rand`` [n, N_samples] / ``u`` [n, N_importance] are the step's random
+        draws (perturb jitter, training-mode fine u); None draws them on the
+        device (t_rand, then u: torch.rand's stream, VR:233, :248).
+        In graph mode the first two steps of a batch shape run eagerly (they
+        create the packers' buffers, Adam's state and the BLAS handles), the
+        third is captured and every step from then on replays the graph with
+        the batch AND the draws copied into its static inputs (no RNG inside the
+        graph: the draws come from the same stream, in the same order, as an
+        eager step's); the returned losses are the graph's output tensors."""
+        if self.graph:
+            return self._step_graphed(rays_o, rays_d, target, t_rand, u, group)
         return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
 
-    def _step_graphed(self, rays_o, rays_d, target, group):
-        key = (rays_o.shape[0], group is not None)
-        g = self._graphs.get(key)
-        if g is None:
-            if self._warm.get(key, 0) < 2:
-                self._warm[key] = self._warm.get(key, 0) + 1
-                return self._step_eager(rays_o, rays_d, target, None, None, group)
-            static = (rays_o.detach().clone(), rays_d.detach().clone(), target.detach().clone())
-            graph = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(graph):
-                out = self._step_eager(*static, None, None, group)
-            g = self._graphs[key] = (graph, static, out)
-        graph, (s_ro, s_rd, s_t), out = g
-        s_ro.copy_(rays_o)
-        s_rd.copy_(rays_d)
-        s_t.copy_(target)
-        graph.replay()
-        return out
-
-    def _step_eager(self, rays_o, rays_d, target, t_rand=None, u=None, group=None):
-        n = rays_o.shape[0]
+    def _draws(self, n, t_rand, u):
         if t_rand is None:
             t_rand = torch.rand((n, self.N_samples), device=self.device)
         if u is None:
             u = torch.rand((n, self.N_importance), device=self.device)
+        return t_rand, u
+
+    def _step_graphed(self, rays_o, rays_d, target, t_rand, u, group):
+        key = (rays_o.shape[0], group is not None)
+        g = self._graphs.get(key)
+        t_rand, u = self._draws(rays_o.shape[0], t_rand, u)
+        if g is None:
+            if self._warm.get(key, 0) < 2:
+                self._warm[key] = self._warm.get(key, 0) + 1
+                return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
+            static = tuple(x.detach().clone().contiguous()
+                           for x in (rays_o, rays_d, target, t_rand, u))
+            graph = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.graph(graph):
+                out = self._step_eager(*static, group)
+            g = self._graphs[key] = (graph, static, out)
+        graph, static, out = g
+        for dst, src in zip(static, (rays_o, rays_d, target, t_rand, u)):
+            dst.copy_(src)
+        graph.replay()
+        return out
+
+    def _step_eager(self, rays_o, rays_d, target, t_rand=None, u=None, group=None):
+        t_rand, u = self._draws(rays_o.shape[0], t_rand, u)
         self.opt.zero_grad(set_to_none=True)
         losses = self.loss(self.forward(rays_o, rays_d, t_rand, u), target)
         losses["loss"].backward()

@@ -19,7 +19,7 @@ import torch
 from src.config import cfg
 from nerfhip import _lib
 from nerfhip.paths import spiral_poses
-from nerfhip.render import NerfPipeline
+from nerfhip.render import NerfPipeline, reference_draws
 
 
 class Renderer:
@@ -159,13 +159,10 @@ class Renderer:
         pose = torch.as_tensor(batch["pose"]).reshape(-1, 4, 4)[0].float()
         K = torch.as_tensor(batch["intrinsics"]).reshape(-1, 3, 3)[0].float()
         self._sync_weights()
-        n = H * W
-        t_rand = None
-        if self.perturb > 0.0:
-            t_rand = torch.rand((n, self.N_samples), device=self.device)
-        u = None
-        if self.N_importance > 0 and self.net.training:
-            u = torch.rand((n, self.N_importance), device=self.device)
+        # the reference's draws in its order: per 2048-ray chunk t_rand (perturb > 0,
+        # also at eval: lego.yaml:22), then u when the net is in training mode
+        t_rand, u = reference_draws(H * W, self.N_samples, self.N_importance,
+                                    float(self.perturb), self.net.training, self.device)
         with torch.no_grad():
             res = self.pipeline.render_image(H, W, pose, K, t_rand=t_rand, u=u)
         out = {}

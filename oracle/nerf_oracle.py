@@ -415,13 +415,14 @@ class RenderConfig:
 
 
 def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
-           grid=None, grid_counter=0, rays=None):
+           grid=None, grid_counter=0, rays=None, return_zall=False):
     """VR:109-216 on the CPU. Returns (dict of maps, final grid_counter).
 
     ``t_rand`` [H*W, N_samples] supplies the stratification draws when
     ``perturb>0``; ``u_fine`` [H*W, N_importance] the training-mode ``u``; ``grid``
     is the ESS occupancy grid (mutated in place by the reference's update rule).
     ``rays`` = (rays_o, rays_d) overrides the camera (used by sharded tests).
+    ``return_zall`` adds ``res["zall"]`` [n, S+NI]: the merged fine depths (VR:183).
     """
     if rays is None:
         rays_o, rays_d = camera_rays(H, W, pose, K)
@@ -430,6 +431,7 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
     n = rays_o.shape[0]
     u_eval = linspace_f32(0.0, 1.0, cfg.N_importance) if cfg.N_importance > 0 else None
     out = {}
+    zalls = []
     counter = grid_counter
     for c0 in range(0, n, cfg.ray_chunk):
         sl = slice(c0, min(n, c0 + cfg.ray_chunk))
@@ -464,6 +466,7 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
                 u = u_eval
             zf = sample_fine(mids, w0[:, 1:-1], u)
             zall = np.sort(np.concatenate([z, zf], -1), -1)
+            zalls.append(zall)
             pts_f = (ro[:, None, :] + rd[:, None, :] * zall[:, :, None]).astype(F32)
             raw_f = query_network(pts_f, rd, params, "model_fine", cfg.chunk_size)
             rgb, disp, acc, _, depth = comp(raw_f, zall)
@@ -474,4 +477,6 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
     for k, v in out.items():
         a = np.concatenate(v, 0)
         res[k] = a.reshape(H, W, 3) if k.startswith("rgb") else a.reshape(H, W)
+    if return_zall and zalls:
+        res["zall"] = np.concatenate(zalls, 0)
     return res, counter

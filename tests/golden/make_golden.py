@@ -13,6 +13,14 @@ numbers it produced.
 
     python tests/golden/make_golden.py            # all fixtures
     python tests/golden/make_golden.py f1 f3      # selected
+    python tests/golden/make_golden.py --zall     # z_<name>.npz: every ray's fine depths
+
+``--zall`` re-renders each fixture (asserting the maps equal the stored ones
+bit for bit) and writes ``z_<name>.npz`` with the reference's fine depths of
+EVERY ray (``zall`` [n, S+NI], the ``t_vals`` the fine composite receives,
+VR:183-193) and, with ERT, each composite call's chunk-wide termination
+decision (``chunk_any`` [calls], VR:1115-1116). The per-ray fine gate uses
+them to attribute every ray outside the reference's own spread to sampling.
 """
 from __future__ import annotations
 
@@ -143,8 +151,14 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
         sh = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
         return bool((torch.cumprod(1.0 - sh, 1) < rend.ert_threshold).any())
 
+    zall_full, any_all = [], []
+
     def rec_c(raw, z, rays_d):
         r = orig_c(raw, z, rays_d)
+        if rend.enable_ert:
+            any_all.append(chunk_any(raw, z, rays_d))
+        if rend.N_importance > 0 and calls["n"] % 2 == 1:
+            zall_full.append(z.detach().numpy().copy())
         if rend.enable_ert and calls["n"] < 2:
             inter["chunk_any_%d" % calls["n"]] = np.array(chunk_any(raw, z, rays_d))
         if calls["n"] == 0:                      # coarse pass of chunk 0
@@ -175,6 +189,16 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
     finally:
         torch.rand = orig_rand
     n = spec["H"] * spec["W"]
+    if ZALL_ONLY:
+        old = np.load(os.path.join(OUT, name + ".npz"))
+        for k, v in out.items():
+            assert np.array_equal(v.numpy(), old["out_" + k], equal_nan=True), (name, k)
+        if zall_full:
+            path = os.path.join(OUT, "z_" + name + ".npz")
+            np.savez_compressed(path, zall=np.concatenate(zall_full, 0),
+                                chunk_any=np.array(any_all, bool))
+            print(f"{path}: {os.path.getsize(path) / 1024:.1f} KiB")
+        return
     rec = dict(
         H=spec["H"], W=spec["W"], pose=pose, K=K,
         w_seed=seed, w_gain=gain, w_alpha_bias=ab, w_digest=params_digest(params),
@@ -203,7 +227,14 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
           f"keys={sorted(out.keys())}")
 
 
+ZALL_ONLY = False
+
+
 def main(argv):
+    global ZALL_ONLY
+    if "--zall" in argv:
+        ZALL_ONLY = True
+        argv = [a for a in argv if a != "--zall"]
     cfg, Network, vr = _import_reference()
     meta = json.load(open(os.path.join(REF, "data/nerf_synthetic/lego/transforms_test.json")))
     frames, angle = meta["frames"], meta["camera_angle_x"]
@@ -213,6 +244,8 @@ def main(argv):
         if not key:
             raise SystemExit(f"unknown fixture {name}")
         capture(key[0], FIXTURES[key[0]], cfg, Network, vr, frames, angle)
+    if ZALL_ONLY:
+        return
     # the lego test poses travel with the repo (bench/tests on the GPU box)
     poses = np.array([f["transform_matrix"] for f in frames], np.float32)
     np.savez_compressed(os.path.join(OUT, "lego_test_cameras.npz"), poses=poses,

@@ -113,8 +113,43 @@ def ray_errors(res, z, n, keys=FINE_KEYS):
     return out
 
 
-def fine_gate(res, z, s):
-    """Evaluate the three criteria above; returns (ok, report dict)."""
+def load_zall(name):
+    """z_<fixture>.npz (make_golden.py --zall): the reference's fine depths of every
+    ray and its per-call chunk termination decisions, or None."""
+    p = os.path.join(GOLDEN, "z_" + name + ".npz")
+    return dict(np.load(p)) if os.path.exists(p) else None
+
+
+REF_CHUNK = 2048
+
+
+def attribute_tail(ratio, z, zref, zall_hip):
+    """(4) Every ray outside GATE_RATIO x the reference's spread must be explained
+    by sampling, not by the MLP or the composite: its fine depths differ from the
+    reference's (VR:239-268 searchsorted / denom-clamp flips move a fine sample), or
+    - with ERT, whose termination rule is chunk-wide (VR:1115-1123) - some ray of
+    its 2048-ray chunk has different fine depths. Given identical depths the fine
+    pass is held to 1e-5 separately (test_fine_pass_given_reference_depths), so a
+    tail ray with identical depths across its chunk would be a kernel defect.
+    Returns (tail rays, unexplained rays, rays with different depths)."""
+    n = ratio.shape[0]
+    zr = zref["zall"].reshape(n, -1)
+    zh = np.asarray(zall_hip).reshape(n, -1)
+    ddiff = (zr != zh).any(-1)
+    expl = ddiff.copy()
+    if bool(z["enable_ert"]):
+        ch = np.arange(n) // REF_CHUNK
+        cd = np.zeros(ch.max() + 1, bool)
+        np.logical_or.at(cd, ch, ddiff)
+        expl |= cd[ch]
+    tail = ratio > GATE_RATIO
+    return tail, tail & ~expl, ddiff
+
+
+def fine_gate(res, z, s, zref=None, zall_hip=None):
+    """Evaluate the three criteria above (and, given the reference's fine depths
+    of every ray `zref` and the implementation's `zall_hip`, the tail attribution
+    of attribute_tail as a fourth); returns (ok, report dict)."""
     n = int(z["H"]) * int(z["W"])
     errs = ray_errors(res, z, n)
     ratio = np.zeros(n)
@@ -135,4 +170,10 @@ def fine_gate(res, z, s):
     ok = (rep["frac_ratio_ok"] >= GATE_FRAC
           and rep["frac_within_tol"] >= rep["ref_self_frac_within_tol_min"] - 0.02
           and p >= min(80.0, rep["ref_self_psnr_median"] - 6.0))
+    if zref is not None and zall_hip is not None:
+        tail, unexpl, ddiff = attribute_tail(ratio, z, zref, zall_hip)
+        rep.update(tail_rays=int(tail.sum()), tail_unexplained=int(unexpl.sum()),
+                   rays_with_other_fine_depths=int(ddiff.sum()),
+                   tail_unexplained_worst_ratio=float(ratio[unexpl].max()) if unexpl.any() else 0.0)
+        ok = ok and not unexpl.any()
     return ok, rep

@@ -116,3 +116,61 @@ def test_written_checkpoint_has_the_reference_layout(tmp_path):
     assert set(ours["optim"]) == set(theirs["optim"])
     assert len(ours["optim"]["param_groups"]) == len(theirs["optim"]["param_groups"])
     assert set(ours["optim"]["param_groups"][0]) == set(theirs["optim"]["param_groups"][0])
+
+
+def test_training_checkpoint_loads_into_reference_optimizer_and_scheduler(tmp_path):
+    """tools/train_lego.py's resume file: the trainer's single-group Adam state
+    re-laid out as the reference's make_optimizer builds it (one group per
+    parameter in named_parameters() order, optimizer.py:8-28) loads with
+    optim.load_state_dict, the ExponentialLR state with scheduler.load_state_dict
+    (lr_scheduler.py:68-79), and the round trip back gives the trainer's state;
+    the model dir holds only files the reference's listing parses."""
+    import torch
+    from nerfhip.checkpoint import (exponential_lr_state, reference_optim_state, save_model,
+                                    single_group_optim_state)
+    from src.models.nerf.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    order = [n for n, _ in net.named_parameters()]
+    names = order[::-1]                                  # the trainer's own order differs
+    params = dict(net.named_parameters())
+    opt = torch.optim.Adam([params[n] for n in names], lr=5e-4, eps=1e-8)
+    for p in net.parameters():
+        p.grad = torch.randn_like(p)
+    opt.step()
+    ref_sd = reference_optim_state(opt, names, order)
+    # the reference's make_optimizer over the same network
+    ref_opt = torch.optim.Adam([{"params": [p], "lr": 5e-4, "weight_decay": 0.0, "eps": 1e-8}
+                                for p in net.parameters()], 5e-4, weight_decay=0.0, eps=1e-8)
+    ref_opt.load_state_dict(ref_sd)
+    for name, p in net.named_parameters():
+        a, b = ref_opt.state[p], opt.state[p]
+        assert torch.equal(a["exp_avg"], b["exp_avg"]) and torch.equal(a["exp_avg_sq"], b["exp_avg_sq"])
+    back = torch.optim.Adam([params[n] for n in names], lr=5e-4, eps=1e-8)
+    back.load_state_dict(single_group_optim_state(ref_opt.state_dict(), names, order))
+    for p in net.parameters():
+        assert torch.equal(back.state[p]["exp_avg"], opt.state[p]["exp_avg"])
+
+    class ExponentialLR(torch.optim.lr_scheduler.LRScheduler):   # lr_scheduler.py:68-79
+        def __init__(self, optimizer, decay_epochs, gamma=0.1, last_epoch=-1):
+            self.decay_epochs, self.gamma = decay_epochs, gamma
+            super().__init__(optimizer, last_epoch)
+
+        def get_lr(self):
+            return [b * self.gamma ** (self.last_epoch / self.decay_epochs) for b in self.base_lrs]
+    sched = ExponentialLR(ref_opt, decay_epochs=500, gamma=0.1)
+    st = exponential_lr_state(5e-4, 0.1, 1000.0, 250, len(order))
+    sched.load_state_dict(st)
+    assert sched.last_epoch == 250 and abs(sched.get_lr()[0] - 5e-4 * 0.1 ** 0.25) < 1e-12
+
+    class _S:
+        def __init__(self, d):
+            self.state_dict = lambda: d
+    model_dir = tmp_path / "model"
+    save_model(_S(net.state_dict()), _S(ref_sd), _S(st), _S({"step": 250}), str(model_dir), 250,
+               last=True)
+    save_model(_S(net.state_dict()), _S(ref_sd), _S(st), _S({"step": 250}), str(model_dir), 250)
+    # net_utils.py:295-297: int(pth.split('.')[0]) for every file but latest.pth
+    assert [int(f.split(".")[0]) for f in os.listdir(model_dir) if f != "latest.pth"] == [250]
+    ck = torch.load(model_dir / "latest.pth", weights_only=True)
+    assert set(ck) == {"net", "optim", "scheduler", "recorder", "epoch"}

@@ -33,19 +33,37 @@ def _free_port():
     return port
 
 
+def fake_render_chunks(chunks, total, with_fine=True):
+    parts = [fake_render(c * nd.REF_CHUNK, min(nd.REF_CHUNK, total - c * nd.REF_CHUNK), with_fine)
+             for c in chunks]
+    if not parts:
+        return {}
+    return {k: torch.cat([p[k] for p in parts], 0) for k in parts[0]}
+
+
 def _worker(rank, world, port, H, W, chunk_aligned, with_fine, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        frame = nd.render_frame_sharded(lambda p0, n: fake_render(p0, n, with_fine), H, W, rank,
-                                        world, torch.device("cpu"), chunk_aligned=chunk_aligned)
+        if chunk_aligned == "interleaved":
+            frame = nd.render_frame_interleaved(
+                lambda cs: fake_render_chunks(cs, H * W, with_fine), H, W, rank, world,
+                torch.device("cpu"))
+        else:
+            frame = nd.render_frame_sharded(lambda p0, n: fake_render(p0, n, with_fine), H, W,
+                                            rank, world, torch.device("cpu"),
+                                            chunk_aligned=chunk_aligned)
         q.put((rank, {k: v.numpy().copy() for k, v in frame.items()}))  # by value, not fd
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("H,W,chunk_aligned,with_fine", [(8, 5, False, True), (7, 3, False, True),
-                                                         (64, 80, True, True), (3, 1000, True, False)])
+                                                         (64, 80, True, True), (3, 1000, True, False),
+                                                         (64, 80, "interleaved", True),
+                                                         (3, 1000, "interleaved", False),
+                                                         (9, 500, "interleaved", True),
+                                                         (2, 3, "interleaved", True)])
 def test_two_rank_frame_equals_single(H, W, chunk_aligned, with_fine):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -78,6 +96,23 @@ def test_band_partition_covers_image():
                     assert p0 % nd.REF_CHUNK == 0
                 seen.extend(range(p0, p0 + n))
             assert seen == list(range(H * W))
+
+
+def test_interleaved_chunk_sets_cover_image():
+    """Chunk c -> rank c mod P: every chunk exactly once, tiles padded to the
+    largest set, and the gather index maps each pixel to its rank's tile row."""
+    for H, W, world in [(800, 800, 8), (800, 800, 3), (5, 7, 8), (100, 100, 2)]:
+        total = H * W
+        nch = -(-total // nd.REF_CHUNK)
+        seen, npix = [], 0
+        for r in range(world):
+            mine, n, pad = nd.chunk_set(H, W, r, world)
+            assert n <= pad and all(c % world == r for c in mine)
+            seen += mine
+            npix += n
+        assert sorted(seen) == list(range(nch)) and npix == total
+        idx = nd.interleave_index(H, W, world, torch.device("cpu"))
+        assert idx.shape == (total,) and len(set(idx.tolist())) == total
 
 
 def _grad_worker(rank, world, port, q):

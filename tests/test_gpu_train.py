@@ -247,3 +247,39 @@ def test_graph_step_trains_and_honours_lr(dev, mlp):
     tr.step(torch.flip(ro, [0]), torch.flip(rd, [0]), gt)
     for a, b in zip(before, tr.parameters()):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("explicit_draws", [True, False])
+def test_graph_step_equals_eager_steps(dev, explicit_draws):
+    """The HIP-graph step (capturable Adam, device lr; draws copied into static
+    inputs) against the eager step from the same weights, batches and draws:
+    6 steps (2 eager warm-ups, the capture, 3 replays), losses and final
+    parameters at the eager trainer's own run-to-run tolerance (the only
+    arithmetic difference is Adam's capturable multi-tensor update vs the
+    fused one). Without explicit draws both consume torch.rand's device stream
+    in the same order (t_rand, then u) from the same seed."""
+    from nerfhip.train import NerfTrainer
+    z, _, ro, rd, _, _, gt = _setup(dev, "x3")
+    g = torch.Generator(device=dev).manual_seed(7)
+    n = ro.shape[0]
+    batches = []
+    for i in range(6):
+        perm = torch.randperm(n, device=dev, generator=g)
+        tr_ = torch.rand((n, 64), device=dev, generator=g) if explicit_draws else None
+        u_ = torch.rand((n, 128), device=dev, generator=g) if explicit_draws else None
+        batches.append((ro[perm], rd[perm], gt[perm], tr_, u_))
+    runs = {}
+    for graph in (False, True):
+        torch.manual_seed(99)
+        tr = NerfTrainer(dev, params_of(z), mlp="x3", graph=graph)
+        losses = []
+        for b in batches:
+            losses.append(float(tr.step(*b)["loss"].item()))
+        runs[graph] = (np.array(losses), {k: v.clone() for k, v in tr.state().items()})
+    assert len(tr._graphs) == 1
+    le, lg = runs[False][0], runs[True][0]
+    assert le[0] == lg[0]                          # identical first forward
+    assert np.all(np.abs(le - lg) <= 1e-5 * np.abs(le)), (le, lg)
+    for k, a in runs[False][1].items():
+        b = runs[True][1][k]
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (k, (a - b).abs().max().item())

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from conftest import golden_names
-from goldlib import MAP_KEYS, fine_gate, grid_of, load, max_err, oracle_cfg, params_of, psnr, rel_err
+from goldlib import (MAP_KEYS, fine_gate, grid_of, load, load_zall, max_err, oracle_cfg, params_of,
+                     psnr, rel_err)
 from oracle import nerf_oracle as O
 
 ALL = golden_names()
@@ -130,9 +131,26 @@ def test_fine_maps_end_to_end_gate(name):
         pytest.skip("coarse-only config")
     res, _ = O.render(int(z["H"]), int(z["W"]), z["pose"], z["K"], params_of(z), oracle_cfg(z),
                       t_rand=z.get("t_rand"), grid=grid_of(z),
-                      grid_counter=int(z["grid_counter_in"]))
-    ok, rep = fine_gate(res, z, load("s_" + name))
+                      grid_counter=int(z["grid_counter_in"]), return_zall=True)
+    ok, rep = fine_gate(res, z, load("s_" + name), load_zall(name), res["zall"])
     assert ok, rep
+    assert rep["tail_unexplained"] == 0, rep
+
+
+@pytest.mark.parametrize("name", [n for n in ALL if not n.startswith("f5")])
+def test_full_fine_depth_fixture_consistent(name):
+    """z_<fixture>.npz (every ray's fine depths, make_golden.py --zall) agrees
+    with the fixture's stored first-chunk intermediates, and the recorded ERT
+    chunk decisions with int_chunk_any_*."""
+    z, zz = load(name), load_zall(name)
+    n = int(z["H"]) * int(z["W"])
+    assert zz["zall"].shape == (n, int(z["N_samples"]) + int(z["N_importance"]))
+    assert np.array_equal(zz["zall"][:z["int_zall"].shape[0]], z["int_zall"])
+    assert np.all(np.diff(zz["zall"], axis=-1) >= 0)           # sorted merge (VR:183)
+    if bool(z["enable_ert"]):
+        assert zz["chunk_any"].shape == (2 * (-(-n // 2048)),)
+        assert bool(zz["chunk_any"][0]) == bool(z["int_chunk_any_0"])
+        assert bool(zz["chunk_any"][1]) == bool(z["int_chunk_any_1"])
 
 
 @pytest.mark.parametrize("name", ALL)

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
-ARGS=${BENCH_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-fp32-run --no-gt --no-c3}
+ARGS=${BENCH_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-fp32-run --no-gt --no-c3 --no-c4}
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 i=0
 for grp in ${PMC_GROUPS:-FETCH_SIZE WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES__GRBM_GUI_ACTIVE__SQ_WAVE_CYCLES__SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT__SQ_INSTS_LDS__SQ_INSTS_VALU_MFMA_F32}; do

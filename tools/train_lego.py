@@ -16,15 +16,22 @@ any GPU at 800x800 with autograd; ray batches are the recipe's own N_rays. The
 iterations.
 
 Images come from data/lego/train.npz (tools/pack_lego.py), white-composited as
-blender.py:60-75 does. Checkpoints are the reference's format
-(nerfhip.checkpoint): ``<out>/latest.pth`` = {net, optim, scheduler, recorder,
-epoch} for resuming, and ``<out>/net/latest.pth`` = {net, epoch} (the weights
-only, what bench.py and the plugin read). At the end the test views of
+blender.py:60-75 does. Checkpoints are the reference's format, written by
+``nerfhip.checkpoint.save_model`` (net_utils.py:323-344) into ``<out>/model/``
+(which holds nothing but ``latest.pth`` and ``<step>.pth``, as the reference's
+``load_model`` listing expects, net_utils.py:295-297): {net, optim, scheduler,
+recorder, epoch} with the optimizer state in the layout of the reference's
+``make_optimizer`` (one param group per parameter, optimizer.py:8-28) and the
+scheduler as its ExponentialLR state (gamma 0.1, decay_epochs = the steps this
+run's schedule takes to decay 10x, last_epoch = step), so the reference's
+``load_model`` resumes from it; ``<out>/net/latest.pth`` = {net, epoch} (the
+weights only, what bench.py and the plugin read); logs and eval files go to
+``<out>/``. At the end the test views of
 data/lego/test.npz are rendered by the HIP inference pipeline and scored with
 the reference evaluator's PSNR (evaluators/nerf.py:465-504).
 
     python tools/train_lego.py --out gpurun_out/lego --max-seconds 1000
-    python tools/train_lego.py --out gpurun_out/lego --resume gpurun_out/lego/latest.pth
+    python tools/train_lego.py --out gpurun_out/lego --resume gpurun_out/lego/model/latest.pth
 """
 import argparse
 import json
@@ -67,7 +74,8 @@ def main():
     args = ap.parse_args()
 
     import torch
-    from nerfhip.checkpoint import load_checkpoint
+    from nerfhip.checkpoint import (exponential_lr_state, load_checkpoint, reference_optim_state,
+                                    save_model, single_group_optim_state)
     from nerfhip.evaluate import load_packed, psnr
     from nerfhip.render import NerfPipeline
     from nerfhip.train import NerfTrainer, camera_rays_at
@@ -76,6 +84,7 @@ def main():
     t_start = time.perf_counter()
     dev = torch.device("cuda:0")
     os.makedirs(os.path.join(args.out, "net"), exist_ok=True)
+    model_dir = os.path.join(args.out, "model")
     imgs, poses, focal, _ = load_packed(os.path.join(args.data, "train.npz"))
     V, H, W, _ = imgs.shape
     images = torch.from_numpy(imgs).to(dev)
@@ -92,11 +101,15 @@ def main():
             init[f"{prefix}.{k}"] = v
     tr = NerfTrainer(dev, init, mlp=args.mlp, detach_fine_samples=args.detach_fine_samples,
                      graph=args.graph)
+    names = [n for n, _ in tr.named_parameters()]
+    from src.models.nerf.network import Network
+    order = [n for n, p in Network().named_parameters() if p.requires_grad]
+    assert sorted(order) == sorted(names), "trainer parameters differ from the Network's"
     step0 = 0
     if args.resume:
         ck = load_checkpoint(args.resume)
         tr.load(ck["net"])
-        tr.opt.load_state_dict(ck["optim"])
+        tr.opt.load_state_dict(single_group_optim_state(ck["optim"], names, order))
         step0 = int(ck["epoch"])
         print(f"resumed {args.resume} at step {step0}", flush=True)
     gamma = math.log(args.lr_final / args.lr) / args.steps
@@ -116,13 +129,19 @@ def main():
         ro, rd = camera_rays_at(poses_d, K, y * W + x, view, W)
         return ro, rd, images[view, y, x]
 
+    class _State:       # what save_model calls state_dict() on
+        def __init__(self, fn):
+            self.state_dict = fn
+
+    decay_epochs = math.log(0.1) / gamma        # steps per 10x decay of this run's schedule
+
     def save(step):
         state = {k: v.detach().cpu() for k, v in tr.state().items()}
-        full = {"net": state, "optim": tr.opt.state_dict(),
-                "scheduler": {"gamma": gamma, "base_lr": args.lr, "steps": args.steps},
-                "recorder": {"step": step}, "epoch": step}
-        torch.save(full, os.path.join(args.out, "latest.pth.tmp"))
-        os.replace(os.path.join(args.out, "latest.pth.tmp"), os.path.join(args.out, "latest.pth"))
+        save_model(_State(lambda: state),
+                   _State(lambda: reference_optim_state(tr.opt, names, order)),
+                   _State(lambda: exponential_lr_state(args.lr, 0.1, decay_epochs, step,
+                                                       len(order))),
+                   _State(lambda: {"step": step}), model_dir, step, last=True)
         torch.save({"net": state, "epoch": step}, os.path.join(args.out, "net", "latest.pth"))
 
     step = step0
