@@ -586,7 +586,7 @@ def torch_cpu_baseline_c1(params, cpu, dev):
         g = pipe.render_image(H, W, pose, K)
     torch.cuda.synchronize()
     t_gpu = (time.perf_counter() - t0) / 5
-    e = float(np.abs(g["rgb_map_0"].cpu().numpy() - ref["rgb_map_0"].numpy().reshape(-1, 3)).max())
+    e = float(np.abs(g["rgb_map_0"].cpu().numpy() - np.asarray(ref["rgb_map_0"]).reshape(-1, 3)).max())
     return {"value": H * W / t_cpu / 1e6, "unit": "Mrays/s", "seconds_per_frame": t_cpu,
             "cores": int(torch.get_num_threads()), "kind": "port",
             "sample": f"one whole lego test view 0 at {H}x{W}, 64 coarse samples, N_importance 0 "

@@ -237,7 +237,7 @@ class NerfTrainer:
 
     def __init__(self, device, params, N_samples=64, N_importance=128, near=2.0, far=6.0,
                  white_bkgd=True, lr=5e-4, clip_value=40.0, mlp="x3",
-                 detach_fine_samples=False, graph=False, ops="hip"):
+                 detach_fine_samples=False, graph=False, ops="hip", adam=None):
         from src.models.nerf.network import NeRF
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -264,7 +264,12 @@ class NerfTrainer:
             raise ValueError("graph=True needs ops='hip' (torch's cumprod backward syncs)")
         self.ops = ops
         self.graph = bool(graph)
-        if self.graph:
+        # adam: "fused" (one fused multi-tensor kernel, the eager default) or
+        # "capturable" (step count and lr on the device; what the graph needs)
+        adam = adam or ("capturable" if self.graph else "fused")
+        if adam not in ("fused", "capturable") or (self.graph and adam != "capturable"):
+            raise ValueError("adam must be 'fused' or 'capturable' (graph: 'capturable')")
+        if adam == "capturable":
             self.opt = torch.optim.Adam(self.parameters(),
                                         lr=torch.tensor(lr, device=self.device), eps=1e-8,
                                         weight_decay=0.0, capturable=True, foreach=True)

@@ -49,10 +49,12 @@ def main():
         capture(name, spec, cfg, Network, vr, meta)
 
 
-def capture(name, SPEC, cfg, Network, vr, meta, params=None, write=True):
+def capture(name, SPEC, cfg, Network, vr, meta, params=None, write=True, full=False):
     """One reference training step; writes tests/golden/<name>.npz (write=True)
     and returns the record. params overrides the spec's generated weights
-    (make_train_sensitivity.py: exact reparametrisations)."""
+    (make_train_sensitivity.py: exact reparametrisations). full: the record
+    also holds every gradient tensor, ``gfull__<param>`` (full loss) and
+    ``gcfull__<param>`` (coarse loss), float64 (make_train_fullgrad.py)."""
     import torch
     frames, angle = meta["frames"], float(meta["camera_angle_x"])
     cfg.task_arg.N_importance = 128
@@ -135,6 +137,10 @@ def capture(name, SPEC, cfg, Network, vr, meta, params=None, write=True):
         if k in coarse_only:
             rec["gcnorm__" + k] = np.float64(coarse_only[k].norm().item())
             rec["gchead__" + k] = coarse_only[k].numpy().reshape(-1)[:64].copy()
+        if full:
+            rec["gfull__" + k] = g.numpy().copy()
+            if k in coarse_only:
+                rec["gcfull__" + k] = coarse_only[k].numpy().copy()
     rec["param_names"] = np.array(names)
     if not write:
         return rec

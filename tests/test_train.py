@@ -105,3 +105,20 @@ def test_composite_ert_matches_oracle_per_chunk(white):
     assert torch.isfinite(t_raw.grad).all()
     g1 = torch.cat([t_raw.grad[2048:2048 + 9], t_raw.grad[2048 + 10:4096]])
     assert (g1 == 0).all()          # chunk 1: every other ray's weights zeroed (quirk 1)
+
+
+@pytest.mark.parametrize("name", ["t1_train_step", "t2_train_ess_ert"])
+def test_full_gradient_fixture_consistent(name):
+    """tg_<name>.npz (make_train_fullgrad.py) holds the golden step's gradients
+    element by element: their norms / sums / first values are the golden's, and
+    the reference's self-distance under reparametrisation is a sane fraction."""
+    from goldlib import load
+    z, tg = load(name), load("tg_" + name)
+    for k in [str(s) for s in z["param_names"]]:
+        g = tg["g__" + k].astype(np.float64)
+        assert abs(np.linalg.norm(g) - float(z["gnorm__" + k])) <= 1e-6 * float(z["gnorm__" + k]) + 1e-12
+        assert np.allclose(g.reshape(-1)[:64], z["ghead__" + k], rtol=0, atol=1e-30 + 1e-7 * np.abs(g).max())
+        assert 0.0 <= float(tg["gdist__" + k]) < 0.2
+        if "gcnorm__" + k in z:
+            gc = tg["gc__" + k].astype(np.float64)
+            assert abs(np.linalg.norm(gc) - float(z["gcnorm__" + k])) <= 1e-6 * float(z["gcnorm__" + k]) + 1e-12
