@@ -198,6 +198,49 @@ typedef struct NerfWgradDesc {
   int M, N;
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
+
+/* nerf_mlp_train_forward_x3: the whole forward of a training step's MLP in ONE
+ *   launch (the inference kernel over the 73-slice stream that keeps the
+ *   feature layer: nerfhip.pack.pack_mlp_x3(fold=False), or its device-side
+ *   packer nerfhip.train_mlp.X3StreamPacker). Samples p = 0 .. P-1 at pts[p]
+ *   ([P][3]) with view direction dirs[p]; `zero` = one device float 0.0.
+ *   raw[p] = (rgb logits, sigma) as nerf_mlp_forward_x3; besides, every
+ *   output is written feature-major with row stride out->ld floats:
+ *   act[L] = h_L (rows 0..255) for L = 0..7, act[8] = feature (256 rows),
+ *   act[9] = the views layer's output (128 rows); bits[L] = the ReLU bits of
+ *   h_L (nerf_x3_layer_ex's layout, m_tiles 16) for L = 0..7 and bits[8] those
+ *   of the views output (m_tiles 8); amax[0..8], amax[11] (device floats,
+ *   caller-initialised, >= 0) are raised to max |h_0..h_7|, max |feature|,
+ *   max |views output| (slots 9, 10 untouched). */
+typedef struct NerfX3TrainOut {
+  float* act[10];
+  unsigned short* bits[9];
+  float* amax;
+  int64_t ld;
+} NerfX3TrainOut;
+int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_head, const float* pts,
+                              const float* dirs, const float* zero, int64_t P,
+                              const NerfX3TrainOut* out, float* raw, nerf_stream_t stream);
+
+/* nerf_mlp_train_backward_x3: the backward through the training MLP (the
+ *   dgrad chain) in ONE launch, over the transposed-weight stream of
+ *   nerfhip.train_mlp.X3BwdStreamPacker (72 slices with_enc, 68 without).
+ *   From io->d_raw ([P][4]: d rgb logits, d sigma; 16-byte aligned) and the
+ *   forward's ReLU bits (io->bits as NerfX3TrainOut.bits), writes with row
+ *   stride io->ld: d[9] = d_hv (128 rows), d[8] = d feature (256), d[7] ..
+ *   d[0] = the gradients of the pre-activations of layers 7 .. 0 (256 rows
+ *   each); with_enc also d[10] / d[11] = the xyz encoding's gradient through
+ *   layer 5 / layer 0 (64 rows; row 63 is padding). io->dmax[0..8], [10]
+ *   (caller-initialised, >= 0) are raised to the outputs' max |.|. */
+typedef struct NerfX3BwdIO {
+  const float* d_raw;
+  const unsigned short* bits[9];
+  float* d[12];
+  float* dmax;
+  int64_t ld;
+} NerfX3BwdIO;
+int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_head, int64_t P,
+                               int with_enc, const NerfX3BwdIO* io, nerf_stream_t stream);
 /* nerf_freq_encode_fm: the frequency encoding of freq.py:7-32 (reference
  *   embed_fn / embeddirs_fn, encoding/__init__.py:7-18), written feature-major
  *   for the training MLP: out[j * ldo + p] for the 3 + 6 * n_freq columns of

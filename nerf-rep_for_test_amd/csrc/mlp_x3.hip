@@ -45,9 +45,13 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 // slice must then be visible one barrier earlier: x3_slice_end certifies slice
 // g+2 at the end of slice g.
 
-// The fragment register sets, live across slices (x: even groups, y: odd).
+// The fragment register sets, live across slices (x: even groups, y: odd),
+// and the stream length (a compile-time constant of each kernel: 65 slices for
+// inference, where the feature layer is folded into the views layer, 73 for
+// the training forward, which keeps it).
 struct FragPipe {
   Frags x, y;
+  int ns;
 };
 
 // The weight stream runs three slices ahead of the compute.
@@ -61,8 +65,9 @@ constexpr int kX3Pieces = 8;   // LDS-DMA pieces per loading wave and slice
 // first, so a tile starts on slices already resident instead of a staged
 // prologue. Measured and dropped (round 2): a half-slice stagger of the SIMD
 // partners, other loader splits and wave priorities, workgroup start skews.
-__device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane) {
-  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4, kX3Slices);
+__device__ __forceinline__ Dma x3_dma(const float4* slices, int t, float* buf, int wave, int lane,
+                                      int ns) {
+  return make_dma_blocks(slices, t, buf, (wave & 3) * 8, wave, lane, wave < 4, ns);
 }
 
 // Group G of NG: drain its fragment reads (issued one group earlier), issue
@@ -118,9 +123,9 @@ __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const
   const int t = g + kX3DmaAhead;
   // the stream runs on into the next tile (the last tile's wrapped pieces are
   // staged but never read): every slice stages one, every slice_end counts 2
-  const int ts = t < kX3Slices ? t : t - kX3Slices;
+  const int ts = t < fp.ns ? t : t - fp.ns;
   run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp,
-                               x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane), hook);
+                               x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane, fp.ns), hook);
 }
 
 // End of slice g: this wave's LDS-DMA of slice g+2 has landed (the next
@@ -166,6 +171,32 @@ struct SplitHook {
   }
 };
 
+// TRAIN: an operand pair of the previous layer's output (FP32, before its split)
+// is written to HBM at the start of the slice that splits it -- before the
+// slice issues its LDS-DMA pieces, so the slice's closing counted vmcnt (which
+// lets the pieces stay in flight) only waits for stores issued a slice
+// earlier. Stores issued after the pieces would make that wait drain the
+// pieces (vmcnt counts loads, stores and LDS-DMA together, in issue order).
+// NoPend: inference (nothing stored).
+struct NoPend {
+  template <int P>
+  __device__ __forceinline__ void pair(const Op&) {}
+};
+
+template <int P, typename Pend, typename Split>
+struct StoreThen {
+  Pend& st;
+  Split sp;
+  template <int G>
+  __device__ __forceinline__ void prefetch() {
+    if constexpr (G == 0) st.template pair<P>(sp.op);
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    sp.template after<G>(acc);
+  }
+};
+
 // two operand splits in one slice (views layer)
 struct Split2 {
   SplitHook a, b;
@@ -175,6 +206,23 @@ struct Split2 {
   __device__ __forceinline__ void after(Acc& acc) {
     a.template after<G>(acc);
     b.template after<G>(acc);
+  }
+};
+
+template <int P, typename Pend>
+struct StoreThen2 {   // views slice: pairs P, P+1 stored, then split
+  Pend& st;
+  Split2 sp;
+  template <int G>
+  __device__ __forceinline__ void prefetch() {
+    if constexpr (G == 0) {
+      st.template pair<P>(sp.a.op);
+      st.template pair<P + 1>(sp.b.op);
+    }
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    sp.template after<G>(acc);
   }
 };
 
@@ -248,12 +296,12 @@ __device__ __forceinline__ void slice256(f32x4 (&acc)[16], const Ring& R, int g,
 }
 
 // A whole epilogue outside a slice (skip layer): each pair's biases, then it.
-template <int P>
-__device__ __forceinline__ void epi_pairs(EpiHook& epi, f32x4 (&acc)[16]) {
+template <int P, typename Epi>
+__device__ __forceinline__ void epi_pairs(Epi& epi, f32x4 (&acc)[16]) {
   if constexpr (P < 8) {
-    epi.prefetch<P>();
+    epi.template prefetch<P>();
     lds_drain();
-    epi.pair<P>(acc);
+    epi.template pair<P>(acc);
     epi_pairs<P + 1>(epi, acc);
   }
 }
@@ -262,44 +310,125 @@ __device__ __forceinline__ void epi_pairs(EpiHook& epi, f32x4 (&acc)[16]) {
 // accumulators, slice q splits operand q+1 (scale s) in its MFMA shadows, the
 // last runs the fused epilogue (disabled for the skip layer, whose two
 // encoding slices follow).
+template <typename Epi, typename Pend>
 __device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int g, Op (&X)[8],
-                                           float s, FragPipe& fp, EpiHook& epi) {
-  { SplitHook h{X[1], s}; slice256x<0, true>(acc, R, g + 0, X, fp, h); }
-  { SplitHook h{X[2], s}; slice256<1>(acc, R, g + 1, X, fp, h); }
-  { SplitHook h{X[3], s}; slice256<2>(acc, R, g + 2, X, fp, h); }
-  { SplitHook h{X[4], s}; slice256<3>(acc, R, g + 3, X, fp, h); }
-  { SplitHook h{X[5], s}; slice256<4>(acc, R, g + 4, X, fp, h); }
-  { SplitHook h{X[6], s}; slice256<5>(acc, R, g + 5, X, fp, h); }
-  { SplitHook h{X[7], s}; slice256<6>(acc, R, g + 6, X, fp, h); }
+                                           float s, FragPipe& fp, Epi& epi, Pend& st) {
+  { StoreThen<1, Pend, SplitHook> h{st, {X[1], s}}; slice256x<0, true>(acc, R, g + 0, X, fp, h); }
+  { StoreThen<2, Pend, SplitHook> h{st, {X[2], s}}; slice256<1>(acc, R, g + 1, X, fp, h); }
+  { StoreThen<3, Pend, SplitHook> h{st, {X[3], s}}; slice256<2>(acc, R, g + 2, X, fp, h); }
+  { StoreThen<4, Pend, SplitHook> h{st, {X[4], s}}; slice256<3>(acc, R, g + 3, X, fp, h); }
+  { StoreThen<5, Pend, SplitHook> h{st, {X[5], s}}; slice256<4>(acc, R, g + 4, X, fp, h); }
+  { StoreThen<6, Pend, SplitHook> h{st, {X[6], s}}; slice256<5>(acc, R, g + 5, X, fp, h); }
+  { StoreThen<7, Pend, SplitHook> h{st, {X[7], s}}; slice256<6>(acc, R, g + 6, X, fp, h); }
   slice256<7>(acc, R, g + 7, X, fp, epi);
   epi.finish(acc);
+}
+
+// ---------------------------------------------------------------------------
+// The training forward (TRAIN): the same kernel over the unfolded 73-slice
+// stream (the feature layer kept: its output and weights are the training
+// step's), which also writes every layer's output FP32 rows to HBM feature-
+// major ([F][P], row stride ld: what the backward's weight gradients read),
+// the ReLU bits of h0..h7 and of the views layer in x3_layer_kernel's mask-bit
+// layout (its dgrad launches read them), and each output's max |.| (the weight
+// gradients' FP16 scales) -- one launch instead of ten x3_layer_kernel
+// launches, the activations never read back from HBM.
+// ---------------------------------------------------------------------------
+// LDS atomic max (the outputs' max |.|: non-negative floats compare as their
+// bits) as inline asm: hipcc places an s_waitcnt vmcnt(0) before any compiler-
+// visible DS instruction while LDS-DMA may be in flight (it cannot prove the
+// addresses apart), which would drain the weight stream's pieces and the
+// activation stores at every layer. Completed by the next lgkmcnt(0) drain.
+__device__ __forceinline__ void lds_max_u32(unsigned* p, unsigned v) {
+  asm volatile("ds_max_u32 %0, %1" ::"v"(lds_addr(reinterpret_cast<const float*>(p))), "v"(v)
+               : "memory");
+}
+
+struct ActStore {
+  __amdgpu_buffer_rsrc_t rs;   // the layer's output rows (num_records: rows * ld * 4)
+  __amdgpu_buffer_rsrc_t rb;   // its ReLU-bit words (num_records 0: no bits)
+  unsigned soff;               // uniform: the tile's first sample of this wave, * 4
+  unsigned sboff;              // uniform: this (tile, wave)'s first bit word, * 2
+  unsigned ld4;                // uniform: row stride in bytes
+  unsigned wb;                 // bits of the current 4-tile block
+  bool bits, valid;
+  // pair G = tiles 2G (v[0..3], rows 32G + 4 g4 + r) and 2G+1 (v[4..7], rows + 16).
+  // The lane's offsets are recomputed here (a few VALU in the MFMA shadows)
+  // instead of living in VGPRs through the whole tile.
+  template <int G>
+  __device__ __forceinline__ void pair(const Op& v) {
+    unsigned lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+    const unsigned vo = valid ? (lid >> 4) * 4u * ld4 + (lid & 15u) * 4u + soff : 0x7fffffffu;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, (int)vo,
+                                            (int)((32 * G + r) * ld4), 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + r]), rs, (int)vo,
+                                            (int)((32 * G + 16 + r) * ld4), 0);
+    }
+    if (bits) {   // bit 4t + r of the block word = (h > 0): post-ReLU h >= 0
+      unsigned m = 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m |= min(__float_as_uint(v[j]), 1u) << j;
+      if constexpr ((G & 1) == 0) {
+        wb = m;
+      } else {
+        wb |= m << 8;
+        if (valid)
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)wb, rb, (int)(lid * 2u),
+                                                (int)(sboff + (G >> 1) * 128), 0);
+      }
+    }
+  }
+};
+
+// Output locations of the training forward (nerf_mlp_train_forward_x3).
+struct X3TrainOut {
+  float* act[10];               // h0..h7, feature, views-layer output (rows, stride ld)
+  unsigned short* bits[9];      // ReLU bits of h0..h7 (x3_layer_kernel MT 16) and views (MT 8)
+  float* amax;                  // [12]: raised to max |.| of h0..h7 (0-7), feature (8), views (11)
+  int64_t ld;                   // row stride of every output, floats
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, int64_t ld) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)((int64_t)rows * ld * 4), 0x00020000);
 }
 
 // LIST: the samples are the flat indices list[0 .. *count) (ray * S + step,
 // written by the ERT segment kernel; the count is read on the device, so a
 // segmented evaluation needs no host round trip); raw is written at those
 // indices. Otherwise the samples are 0 .. total.
-template <bool LIST>
-__global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
+template <bool LIST, bool TRAIN>
+__device__ __forceinline__ void mlp_x3_body(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
-    float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count) {
+    float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count,
+    const X3TrainOut& to) {
   if constexpr (LIST) total = *count;
   __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
   __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
+  __shared__ unsigned amax_lds[12];   // TRAIN: this workgroup's max |.| per output
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   Ring R{ring, slices, wave, lane};
+  constexpr int kNs = TRAIN ? NERF_MLP_SLICES : kX3Slices;
 
-  for (int t = 0; t < kX3DmaAhead; ++t)
-    stage_slice(make_dma(slices, t, R.buf(t), wave, lane));   // all 8 waves, 4 pieces each
+  for (int t = 0; t < kX3DmaAhead; ++t)   // all 8 waves, 4 pieces each
+    stage_slice(TRAIN ? make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane,
+                                        true, kNs)
+                      : make_dma(slices, t, R.buf(t), wave, lane));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
+  if constexpr (TRAIN) {
+    if (tid < 12) amax_lds[tid] = 0u;
+  }
 
   FragPipe fp;
+  fp.ns = kNs;
   const int64_t ntiles = (total + kX3Tile - 1) / kX3Tile;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const bool first_tile = tile == (int64_t)blockIdx.x;
@@ -324,6 +453,38 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   encode_xyz(p, g4, encf);
   const float enc_max = sample_max(fmaxf(op_absmax(encf[0]), op_absmax(encf[1])));
 
+  using Epi = EpiHook;   // (the training stores ride on the next slices' hooks)
+  using Pend = typename std::conditional<TRAIN, ActStore, NoPend>::type;
+  // TRAIN: where this (tile, wave) writes (uniform parts; the lane's own part is
+  // recomputed at each store)
+  auto store_for = [&](int L, int rows) {
+    Pend st;
+    if constexpr (TRAIN) {
+      const int wv = __builtin_amdgcn_readfirstlane(wave);
+      // the layer's pointers are loaded from the kernel arguments here, at the
+      // layer (an opaque index: kept live through the whole tile loop, the 19
+      // pointers would not fit the SGPR budget)
+      int Li = L;
+      asm volatile("" : "+s"(Li));
+      st.rs = rows_rsrc(to.act[Li], rows, to.ld);
+      st.bits = L < 8;
+      st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)to.bits[Li < 8 ? Li : 0], 0,
+                                                L < 8 ? 0x7fffffff : 0, 0x00020000);
+      st.soff = (unsigned)((tile * kX3Tile + wv * 16) * 4);
+      st.sboff = (unsigned)(((tile * 8 + wv) * 4) * 64 * 2);
+      st.ld4 = (unsigned)(to.ld * 4);
+      st.wb = 0u;
+      st.valid = valid;
+    } else {
+      (void)L;
+      (void)rows;
+    }
+    return st;
+  };
+  auto amax_to_lds = [&](int slot, float mx) {
+    if constexpr (TRAIN) lds_max_u32(&amax_lds[slot], __float_as_uint(mx));
+  };
+
   f32x4 acc[16];   // every layer's first slice starts it from zero
   Op X[8];
   if (first_tile) __syncthreads();   // head, z/rays loads and the three prologue slices resident
@@ -341,25 +502,30 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     split_op(E[1], s);
     NoHook nh;
     slice256x<0, true>(acc, R, 0, E, fp, nh);
-    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 0] + e)), 0.0f,
-                lds_addr(hd + kHeadBias + g4 * 64), nullptr, 0.0f, 0.0f, true};
+    Epi epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 0] + e)), 0.0f,
+            lds_addr(hd + kHeadBias + g4 * 64), nullptr, 0.0f, 0.0f, true};
     slice256<1>(acc, R, 1, E, fp, epi);
     epi.finish(acc);
+    amax_to_lds(0, epi.amax);
     e = act_exponent(sample_max(epi.amax));
   }
+  // TRAIN: h0 goes to HBM pair by pair in the next layer's slices (pair 0 now)
+  Pend st = store_for(0, 256);
+  st.template pair<0>(X[0]);
   s = ldexpf(1.0f, e);
   split_op(X[0], s);
   int g = 2;
 
   float alpha = 0.0f;
-  // ---- layers 1..7 (skip input at 5) + feature (8, no ReLU) ----------------
-  // (the feature layer, NET:63, has no activation: pack_mlp_x3 folds it into the
-  // views layer, which then reads h7 directly)
+  float mx7 = 0.0f;
+  // ---- layers 1..7 (skip input at 5) ------------------------------------------
+  // (inference: the feature layer, NET:63, has no activation, and pack_mlp_x3
+  // folds it into the views layer, which then reads h7 directly)
   for (int L = 1; L <= 7; ++L) {
-    EpiHook epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)), 0.0f,
-                lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
-                L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
-    act_slices(acc, R, g, X, s, fp, epi);
+    Epi epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + L] + e)), 0.0f,
+            lds_addr(hd + kHeadBias + L * 256 + g4 * 64),
+            L == 7 ? hd + kHeadAlphaW + g4 * 64 : nullptr, 0.0f, 0.0f, L != 5};
+    act_slices(acc, R, g, X, s, fp, epi, st);   // stores h_{L-1} pairs 1..7
     g += 8;
     if (L == 5) {   // cat(input_pts, h) (NET:57-58): the encoding's K steps last
       NoHook nh;
@@ -369,11 +535,17 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
       epi.on = true;   // this layer's epilogue, not pipelined
       epi_pairs<0>(epi, acc);
     }
+    amax_to_lds(L, epi.amax);
     if (L == 7) alpha = quad_sum(epi.apart) + hd[kHeadAlphaB];   // NET:61
     // the next layer's input scale (the skip layer's covers the encoding too)
     float mx = epi.amax;
     if (L == 4) mx = fmaxf(mx, enc_max);
-    if (L == 7) break;
+    st = store_for(L, 256);
+    st.template pair<0>(X[0]);
+    if (L == 7) {
+      mx7 = mx;
+      break;
+    }
     e = act_exponent(sample_max(mx));
     s = ldexpf(1.0f, e);
     split_op(X[0], s);
@@ -383,9 +555,24 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     }
   }
   // acc holds zeros; X holds h7 (FP32, unsplit)
+  if constexpr (TRAIN) {
+    // ---- the feature layer (NET:63): 256 -> 256, no activation -------------
+    e = act_exponent(sample_max(mx7));
+    s = ldexpf(1.0f, e);
+    split_op(X[0], s);
+    Epi epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 8] + e)), -__builtin_inff(),
+            lds_addr(hd + kHeadBias + 8 * 256 + g4 * 64), nullptr, 0.0f, 0.0f, true};
+    act_slices(acc, R, g, X, s, fp, epi, st);   // stores h7 pairs 1..7
+    g += 8;
+    amax_to_lds(8, epi.amax);
+    st = store_for(8, 256);                     // the feature rows: the views slices
+    st.template pair<0>(X[0]);
+    st.template pair<1>(X[1]);
+  }
+  (void)mx7;
 
-  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67),
-  // with feature = W_f h7 + b_f folded in: W_views,feat W_f on h7 ------------
+  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67);
+  // inference: feature = W_f h7 + b_f folded in (W_views,feat W_f on h7) ---------
   Op dirf;
   encode_dir(dv, g4, dirf);
   {
@@ -400,11 +587,11 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
   f32x4 acc8[8];   // started from zero by the first views slice
   {
     // views slice k reads operands 2k, 2k+1 and splits 2k+2, 2k+3 (then dir)
-    Split2 h0{{X[2], s}, {X[3], s}};
+    StoreThen2<2, Pend> h0{st, {{X[2], s}, {X[3], s}}};
     run_slice3<8, StepViews<0, true>>(acc8, R, g, X, fp, h0); x3_slice_end<2>(fp);
-    Split2 h1{{X[4], s}, {X[5], s}};
+    StoreThen2<4, Pend> h1{st, {{X[4], s}, {X[5], s}}};
     run_slice3<8, StepViews<2>>(acc8, R, g + 1, X, fp, h1); x3_slice_end<2>(fp);
-    Split2 h2{{X[6], s}, {X[7], s}};
+    StoreThen2<6, Pend> h2{st, {{X[6], s}, {X[7], s}}};
     run_slice3<8, StepViews<4>>(acc8, R, g + 2, X, fp, h2); x3_slice_end<2>(fp);
     SplitHook h3{dirf, s};
     run_slice3<8, StepViews<6>>(acc8, R, g + 3, X, fp, h3); x3_slice_end<2>(fp);
@@ -421,6 +608,30 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
       for (int r = 0; r < 4; ++r)
         acc8[m][r] = fmaxf(__builtin_fmaf(acc8[m][r], inv, bias[4 * m + r]), 0.0f);
   }
+  if constexpr (TRAIN) {   // the views output rows, its ReLU bits (MT 8) and max
+    int i9 = 9;
+    asm volatile("" : "+s"(i9));
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i9], 128, to.ld);
+    const unsigned ld4 = (unsigned)(to.ld * 4);
+    const unsigned voff = valid ? (unsigned)(((int64_t)4 * g4 * to.ld + gs) * 4) : 0x7fffffffu;
+    float vmax = 0.0f;
+#pragma unroll
+    for (int u0 = 0; u0 < 8; u0 += 4) {
+      unsigned wb = 0u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc8[u0 + t][r];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff,
+                                                (int)((16 * (u0 + t) + r) * ld4), 0);
+          wb |= min(__float_as_uint(v), 1u) << (4 * t + r);
+          vmax = fmaxf(vmax, v);
+        }
+      if (valid) to.bits[i9 - 1][(((tile * 8 + wave) * 8 + u0) / 4) * 64 + lane] = (unsigned short)wb;
+    }
+    amax_to_lds(11, vmax);
+  }
 
   // ---- rgb head (NET:68-70), FP32 on the VALU --------------------------------
   float part[3] = {0.0f, 0.0f, 0.0f};
@@ -435,10 +646,398 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
 #pragma unroll
   for (int c = 0; c < 3; ++c) rgb[c] = quad_sum(part[c]) + hd[kHeadRgbB + c];
   if (valid && g4 == 0) raw[gc] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
-  R.rot = (R.rot + kX3Slices) & 3;   // the next tile's slice 0 = this stream's slice 65
+  R.rot = (R.rot + kNs) & 3;   // the next tile's slice 0 = this stream's slice kNs
   }
   // the last tile's wrapped DMA pieces land before the workgroup's LDS is freed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (TRAIN) {   // one global max per output and workgroup
+    __syncthreads();
+    // (wave, lane), not threadIdx: the thread id is not kept live through the loop
+    float* am = to.amax;
+    asm volatile("" : "+s"(am));
+    if (__builtin_amdgcn_readfirstlane(wave) == 0 && lane < 12)
+      atomicMax(reinterpret_cast<unsigned*>(am) + lane, amax_lds[lane]);
+  }
+}
+
+template <bool LIST>
+__global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
+    const float4* __restrict__ slices, const float* __restrict__ head,
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+    const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
+    float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count) {
+  mlp_x3_body<LIST, false>(slices, head, rays_o, rays_d, z, z_stride, total, S, raw, list, count,
+                           X3TrainOut{});
+}
+
+// The training forward: samples p = 0 .. P-1 at pts[p] with view direction
+// dirs[p] (rays_o = pts, rays_d = dirs, one shared zero depth: o + d * 0 = o).
+__global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_train_kernel(
+    const float4* __restrict__ slices, const float* __restrict__ head,
+    const float* __restrict__ pts, const float* __restrict__ dirs, const float* __restrict__ zero,
+    int64_t P, float4* __restrict__ raw, const X3TrainOut to) {
+  mlp_x3_body<false, true>(slices, head, pts, dirs, zero, 0, P, 1, raw, nullptr, nullptr, to);
+}
+
+
+// ===========================================================================
+// The training backward through the MLP (the dgrad chain) in ONE launch: the
+// inference kernel's per-tile body run through the transposed weights, from
+// the loss gradient d raw [P][4] down to the encoding. Per 128-sample tile:
+//   d_hv = (W_rgb^T d_rgb) * (hv > 0)                 (VALU, FP32; 128 rows)
+//   DF   = W_views[:, :256]^T d_hv                    (4 slices)
+//   D7   = (W_feat^T DF + W_alpha^T d_sigma) * (h7 > 0)    (8 slices)
+//   D_{i-1} = (W_i^T D_i) * (h_{i-1} > 0), i = 7 .. 1 (8 slices each; at i = 5
+//   the h4 rows of W_5, with ENC first d_enc5 = W_5[:, :63]^T D5, 2 slices)
+//   ENC: d_enc0 = W_0^T D0                            (2 slices)
+// (network.py:49-74's autograd; the layer launches of the unfused backward
+// compute the same products). Every output is written feature-major (the weight
+// gradients read them) and its max |.| raised (their FP16 scales). The ReLU
+// masks are the forward's bits, loaded one slice before the epilogue that
+// applies them. Stream (pack: nerfhip.train_mlp.X3BwdStreamPacker): W_views^T
+// (4), W_feat^T (8), W_7^T, W_6^T (8 each), [W_5,enc^T (2)], W_5,h^T, W_4^T ..
+// W_1^T (8 each), [W_0^T (2)]: 72 slices with ENC, 68 without.
+// ===========================================================================
+constexpr int kBwdScales = 3100;   // per-matrix weight scale exponents [11] in the head
+
+struct X3BwdIO {
+  const float4* d_raw;            // [P]: d rgb logits (x, y, z), d sigma (w)
+  const unsigned short* bits[9];  // ReLU bits of h0..h7 (m_tiles 16), of the views output (8)
+  float* d[12];                   // 0..7: D0..D7, 8: DF, 9: d_hv, 10: d_enc (layer 5), 11: (layer 0)
+  float* dmax;                    // raised: [i] = max |D_i|, [8] max |DF|, [10] max |d_hv|
+  int64_t ld;
+};
+
+// Epilogue of a dgrad layer, fused into its last slice: 2^-shift * acc (exact),
+// (+ rank-1 alpha-head term W_alpha[m] * d_sigma, layer 7), * mask bit; running
+// |max|; into X[G] (FP32) for the next layer.
+template <bool RANK1, bool MASK>
+struct BwdEpi {
+  Op (&X)[8];
+  float inv;
+  unsigned aw;          // LDS byte address of the lane group's packed alpha weights (RANK1)
+  float dsig;
+  float amax;
+  unsigned mlds;        // LDS byte address of this lane's mask word of block 0 (MASK)
+  unsigned mw[4];       // the mask words of the 4 tile blocks, read from LDS in the slice
+  f32x4 bb[2][2];
+  template <int G>
+  __device__ __forceinline__ void prefetch() {
+    if constexpr (MASK && (G & 1) == 0 && G < 8)   // drained with the next group's fragments
+      asm volatile("ds_read_u16 %0, %1 offset:%2" : "=v"(mw[G >> 1]) : "v"(mlds), "i"(64 * G)
+                   : "memory");
+    if constexpr (RANK1 && G < 8) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bb[G & 1][0]) : "v"(aw), "i"(32 * G) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bb[G & 1][1]) : "v"(aw), "i"(32 * G + 16) : "memory");
+    }
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    if constexpr (G >= 1 && G <= 8) pair<G - 1>(acc);
+  }
+  template <typename Acc>
+  __device__ __forceinline__ void finish(Acc& acc) {
+    lds_drain();
+    pair<7>(acc);
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void pair(Acc& acc) {
+    Op v;
+    unsigned m = 0xffu;
+    if constexpr (MASK) m = mw[G >> 1] >> (8 * (G & 1));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = acc[2 * G][r] * inv, b = acc[2 * G + 1][r] * inv;   // exact: power of two
+      if constexpr (RANK1) {
+        a = __builtin_fmaf(bb[G & 1][0][r], dsig, a);
+        b = __builtin_fmaf(bb[G & 1][1][r], dsig, b);
+      }
+      v[r] = ((m >> r) & 1u) ? a : 0.0f;
+      v[4 + r] = ((m >> (4 + r)) & 1u) ? b : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j += 2)
+      asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(amax) : "v"(v[j]), "v"(v[j + 1]));
+    asm volatile("" : "+v"(v), "+v"(amax));
+    X[G] = v;
+  }
+};
+
+// The mask words of one layer's ReLU bits for this (tile, wave): 4 x 64 u16
+// (x3_layer_kernel's MT 16 layout, 512 B contiguous) staged into the wave's
+// LDS area by two LDS-DMA dwords per lane, a slice before the epilogue that
+// reads them (an ordinary load's result would make hipcc wait with a vmcnt
+// that ignores LDS-DMA, i.e. drain the weight stream). The loader waves' slice
+// end certifies them (they are older than that slice's pieces); the other
+// waves wait vmcnt(0) at the end of the slice (wait_nonloader).
+struct MaskSrc {
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned soff;        // uniform: ((tile * 8 + wave) * 4 * 64) * 2
+  float* dst;           // this wave's 512-B LDS area
+  __device__ __forceinline__ void load() const {
+    unsigned lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 4, (int)(lid * 4u), (int)soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + 64), 4, (int)(lid * 4u),
+                                             (int)(soff + 256), 0, 0);
+  }
+};
+
+// slice hook: the previous output's pair P stored, the epilogue's masks loaded
+// (both before the slice's DMA pieces), then an operand split
+template <int P, typename Pend, typename Split>
+struct StoreMaskThen {
+  Pend& st;
+  Split sp;
+  const MaskSrc& ms;
+  bool loader;          // wave-uniform: this wave stages weight pieces (waves 0-3)
+  template <int G>
+  __device__ __forceinline__ void prefetch() {
+    if constexpr (G == 0) {
+      if constexpr (P >= 0) st.template pair<P>(sp.op);
+      ms.load();
+    }
+  }
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    sp.template after<G>(acc);
+    if constexpr (G == 7) {
+      if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+};
+struct NoSplit {   // operands already split (the D4 pass after the encoding rows)
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc&) {}
+};
+
+// The 8 slices of a 256-row dgrad layer over operand array X: slice q stores the
+// previous output's pair q+1 and splits operand q+1 (unless PRESPLIT), slice 6
+// also loads the masks, slice 7 runs the epilogue.
+template <bool PRESPLIT, typename Epi, typename Pend>
+__device__ __forceinline__ void dgrad_slices(f32x4 (&acc)[16], const Ring& R, int g, Op (&X)[8],
+                                             float s, FragPipe& fp, Epi& epi, Pend& st,
+                                             const MaskSrc& ms) {
+  if constexpr (PRESPLIT) {
+    NoHook nh;
+    slice256x<0, true>(acc, R, g + 0, X, fp, nh);
+    slice256<1>(acc, R, g + 1, X, fp, nh);
+    slice256<2>(acc, R, g + 2, X, fp, nh);
+    slice256<3>(acc, R, g + 3, X, fp, nh);
+    slice256<4>(acc, R, g + 4, X, fp, nh);
+    slice256<5>(acc, R, g + 5, X, fp, nh);
+    { StoreMaskThen<-1, Pend, NoSplit> h{st, {}, ms, R.wave < 4};
+      slice256<6>(acc, R, g + 6, X, fp, h); }
+  } else {
+    { StoreThen<1, Pend, SplitHook> h{st, {X[1], s}}; slice256x<0, true>(acc, R, g + 0, X, fp, h); }
+    { StoreThen<2, Pend, SplitHook> h{st, {X[2], s}}; slice256<1>(acc, R, g + 1, X, fp, h); }
+    { StoreThen<3, Pend, SplitHook> h{st, {X[3], s}}; slice256<2>(acc, R, g + 2, X, fp, h); }
+    { StoreThen<4, Pend, SplitHook> h{st, {X[4], s}}; slice256<3>(acc, R, g + 3, X, fp, h); }
+    { StoreThen<5, Pend, SplitHook> h{st, {X[5], s}}; slice256<4>(acc, R, g + 4, X, fp, h); }
+    { StoreThen<6, Pend, SplitHook> h{st, {X[6], s}}; slice256<5>(acc, R, g + 5, X, fp, h); }
+    { StoreMaskThen<7, Pend, SplitHook> h{st, {X[7], s}, ms, R.wave < 4};
+      slice256<6>(acc, R, g + 6, X, fp, h); }
+  }
+  slice256<7>(acc, R, g + 7, X, fp, epi);
+  epi.finish(acc);
+}
+
+template <bool ENC>
+__global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
+    const float4* __restrict__ slices, const float* __restrict__ head, int64_t P,
+    const X3BwdIO io) {
+  __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
+  __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
+  __shared__ unsigned dmax_lds[11];
+  __shared__ __attribute__((aligned(16))) float mask_lds[8 * 128];   // 512 B per wave
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  Ring R{ring, slices, wave, lane};
+  constexpr int kNs = ENC ? 72 : 68;
+  for (int t = 0; t < kX3DmaAhead; ++t)   // all 8 waves, 4 pieces each
+    stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, kNs));
+  for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
+    reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
+  if (tid < 11) dmax_lds[tid] = 0u;
+
+  FragPipe fp;
+  fp.ns = kNs;
+  const int64_t ntiles = (P + kX3Tile - 1) / kX3Tile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const bool first_tile = tile == (int64_t)blockIdx.x;
+  const int64_t gs = tile * kX3Tile + wave * 16 + (lane & 15);
+  int g4 = lane >> 4;
+  asm volatile("" : "+v"(g4));
+  const bool valid = gs < P;
+  const int64_t gl = valid ? gs : P - 1;
+  // samples past P: d raw 0, so every product of theirs is 0 whatever the
+  // (unwritten) mask words of their tile say, and no max |.| sees them
+  float4 dr = io.d_raw[gl];
+  if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  // outputs / masks of this (tile, wave): pointers loaded at their layer
+  auto store_for = [&](int k, int rows) {
+    ActStore st;
+    int ki = k;
+    asm volatile("" : "+s"(ki));
+    st.rs = rows_rsrc(io.d[ki], rows, io.ld);
+    st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
+    st.soff = (unsigned)((tile * kX3Tile + wave * 16) * 4);
+    st.sboff = 0u;
+    st.ld4 = (unsigned)(io.ld * 4);
+    st.wb = 0u;
+    st.bits = false;
+    st.valid = valid;
+    return st;
+  };
+  auto mask_for = [&](int L) {
+    int li = L;
+    asm volatile("" : "+s"(li));
+    return MaskSrc{__builtin_amdgcn_make_buffer_rsrc((void*)io.bits[li], 0, 0x7fffffff, 0x00020000),
+                   (unsigned)(((tile * 8 + wave) * 4 * 64) * 2), mask_lds + wave * 128};
+  };
+  auto amax_to_lds = [&](int slot, float mx) { lds_max_u32(&dmax_lds[slot], __float_as_uint(mx)); };
+
+  const unsigned mlane = lds_addr(mask_lds + wave * 128) + lane * 2u;   // block k: + 128 k
+  f32x4 acc[16];
+  Op X[8];
+  if (first_tile) __syncthreads();   // head, d raw and the three prologue slices resident
+  load_frags<0>(fp.x, lds_base(R.buf(0), lane));
+
+  // ---- d_hv = (W_rgb^T d_rgb) * (hv > 0), NET:68-70 backward, FP32 on the VALU
+  {
+    int i8 = 8;
+    asm volatile("" : "+s"(i8));
+    const unsigned short* bv = io.bits[i8];
+    const int64_t wv0 = ((tile * 8 + wave) * 2) * 64 + lane;     // views bits: MT 8
+    const unsigned mv0 = bv[wv0], mv1 = bv[wv0 + 64];
+    const float* wr = hd + kHeadRgbW + g4 * 32;
+    float mx = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = 2 * q + (j >> 2), r = j & 3;
+        float v = wr[4 * m + r] * dr.x;                        // sum over c in order
+        v = __builtin_fmaf(wr[128 + 4 * m + r], dr.y, v);
+        v = __builtin_fmaf(wr[256 + 4 * m + r], dr.z, v);
+        const unsigned mw = m < 4 ? mv0 : mv1;
+        v = ((mw >> (4 * (m & 3) + r)) & 1u) ? v : 0.0f;
+        X[4 + q][j] = v;   // operands 4..7: the last slice reads only X[7]
+        mx = fmaxf(mx, fabsf(v));
+      }
+    ActStore sv = store_for(9, 128);
+    sv.template pair<0>(X[4]);
+    sv.template pair<1>(X[5]);
+    sv.template pair<2>(X[6]);
+    sv.template pair<3>(X[7]);
+    amax_to_lds(10, mx);
+    const int e = act_exponent(sample_max(mx));
+    const float s = ldexpf(1.0f, e);
+    split_op(X[4], s);
+    // ---- DF = W_views[:, :256]^T d_hv (4 slices over operands 4..7, so the
+    // epilogue's writes of X[0..6] in the last slice miss its operand; the view
+    // encoding rows are not needed: view directions are constants)
+    BwdEpi<false, false> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + 0] + e)), 0u, 0.0f, 0.0f};
+    { SplitHook h{X[5], s}; slice256x<4, true>(acc, R, 0, X, fp, h); }
+    { SplitHook h{X[6], s}; slice256<5>(acc, R, 1, X, fp, h); }
+    { SplitHook h{X[7], s}; slice256<6>(acc, R, 2, X, fp, h); }
+    slice256<7>(acc, R, 3, X, fp, epi);
+    epi.finish(acc);
+    amax_to_lds(8, epi.amax);
+  }
+  ActStore st = store_for(8, 256);   // DF rows: pair 0 now, 1..7 in the next slices
+  st.template pair<0>(X[0]);
+  int g = 4;
+  float mx = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) mx = fmaxf(mx, op_absmax(X[q]));
+  int e = act_exponent(sample_max(mx));
+  float s = ldexpf(1.0f, e);
+  split_op(X[0], s);
+  {   // ---- D7 = (W_feat^T DF + W_alpha^T d_sigma) * (h7 > 0) (NET:61, 63)
+    BwdEpi<true, true> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + 1] + e)),
+                           lds_addr(hd + kHeadAlphaW + g4 * 64), dr.w, 0.0f, mlane};
+    const MaskSrc ms = mask_for(7);
+    dgrad_slices<false>(acc, R, g, X, s, fp, epi, st, ms);
+    g += 8;
+    amax_to_lds(7, epi.amax);
+    mx = epi.amax;
+  }
+  // ---- D_{i-1} = (W_i^T D_i) * (h_{i-1} > 0), i = 7 .. 1 ---------------------
+  for (int i = 7; i >= 1; --i) {
+    st = store_for(i, 256);           // D_i rows
+    st.template pair<0>(X[0]);
+    e = act_exponent(sample_max(mx));
+    s = ldexpf(1.0f, e);
+    const int sidx = i >= 6 ? 9 - i : (i == 5 ? 5 : 10 - i);   // W7 2, W6 3, W5h 5, W4 6 .. W1 9
+    BwdEpi<false, true> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + sidx] + e)), 0u, 0.0f, 0.0f,
+                            mlane};
+    const MaskSrc ms = mask_for(i - 1);
+    if (ENC && i == 5) {
+      // the encoding rows first (they read D5 too): D5 stored and split whole
+      st.template pair<1>(X[1]); st.template pair<2>(X[2]); st.template pair<3>(X[3]);
+      st.template pair<4>(X[4]); st.template pair<5>(X[5]); st.template pair<6>(X[6]);
+      st.template pair<7>(X[7]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) split_op(X[q], s);
+      NoHook nh;
+      run_slice3<8, StepEnc4<0, true>>(acc, R, g, X, fp, nh); x3_slice_end<2>(fp);
+      run_slice3<8, StepEnc4<4>>(acc, R, g + 1, X, fp, nh); x3_slice_end<2>(fp);
+      g += 2;
+      {   // d_enc5 = 2^-shift acc (rows 0..63), straight to HBM
+        ActStore se = store_for(10, 64);
+        const float inv = ldexpf(1.0f, -((int)hd[kBwdScales + 4] + e));
+        Op v0, v1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] = acc[0][r] * inv; v0[4 + r] = acc[1][r] * inv;
+          v1[r] = acc[2][r] * inv; v1[4 + r] = acc[3][r] * inv;
+        }
+        se.template pair<0>(v0);
+        se.template pair<1>(v1);
+      }
+      dgrad_slices<true>(acc, R, g, X, s, fp, epi, st, ms);
+    } else {
+      split_op(X[0], s);
+      dgrad_slices<false>(acc, R, g, X, s, fp, epi, st, ms);
+    }
+    g += 8;
+    amax_to_lds(i - 1, epi.amax);
+    mx = epi.amax;
+  }
+  // X holds D0 (FP32)
+  st = store_for(0, 256);
+  st.template pair<0>(X[0]); st.template pair<1>(X[1]); st.template pair<2>(X[2]);
+  st.template pair<3>(X[3]); st.template pair<4>(X[4]); st.template pair<5>(X[5]);
+  st.template pair<6>(X[6]); st.template pair<7>(X[7]);
+  if constexpr (ENC) {   // ---- d_enc0 = W_0^T D0 (64 rows)
+    e = act_exponent(sample_max(mx));
+    s = ldexpf(1.0f, e);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) split_op(X[q], s);
+    NoHook nh;
+    run_slice3<8, StepEnc4<0, true>>(acc, R, g, X, fp, nh); x3_slice_end<2>(fp);
+    run_slice3<8, StepEnc4<4>>(acc, R, g + 1, X, fp, nh); x3_slice_end<2>(fp);
+    ActStore se = store_for(11, 64);
+    const float inv = ldexpf(1.0f, -((int)hd[kBwdScales + 10] + e));
+    Op v0, v1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v0[r] = acc[0][r] * inv; v0[4 + r] = acc[1][r] * inv;
+      v1[r] = acc[2][r] * inv; v1[4 + r] = acc[3][r] * inv;
+    }
+    se.template pair<0>(v0);
+    se.template pair<1>(v1);
+  }
+  R.rot = (R.rot + kNs) & 3;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* dm = io.dmax;
+  asm volatile("" : "+s"(dm));
+  if (wave == 0 && lane < 11 && lane != 9)
+    atomicMax(reinterpret_cast<unsigned*>(dm) + lane, dmax_lds[lane]);
 }
 
 
@@ -1204,6 +1803,75 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
                      z_stride, total, S, (float4*)raw, nullptr, nullptr);
   return check_launch("mlp_x3_kernel");
+}
+
+extern "C" int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_head,
+                                         const float* pts, const float* dirs, const float* zero,
+                                         int64_t P, const NerfX3TrainOut* out, float* raw,
+                                         nerf_stream_t stream) {
+  NERF_REQUIRE(w_slices && w_head && pts && dirs && zero && out && raw && out->amax,
+               "nerf_mlp_train_forward_x3: null pointer");
+  NERF_REQUIRE(P >= 0 && out->ld >= P, "nerf_mlp_train_forward_x3: bad size");
+  for (int i = 0; i < 10; ++i)
+    NERF_REQUIRE(out->act[i] != nullptr, "nerf_mlp_train_forward_x3: null output rows");
+  for (int i = 0; i < 9; ++i)
+    NERF_REQUIRE(out->bits[i] != nullptr, "nerf_mlp_train_forward_x3: null relu bits");
+  NERF_REQUIRE((int64_t)256 * out->ld * 4 < (1ll << 31),
+               "nerf_mlp_train_forward_x3: rows too long for 32-bit offsets");
+  NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
+                   ((uintptr_t)raw & 15) == 0,
+               "nerf_mlp_train_forward_x3: weights/raw must be 16-byte aligned");
+  if (P == 0) return 0;
+  const int64_t blocks = cdiv(P, kX3Tile);
+  NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_train_forward_x3: too many samples");
+  const int n_cu = stream_cu_count(stream);
+  const int64_t grid = blocks < n_cu ? blocks : n_cu;
+  X3TrainOut to;
+  for (int i = 0; i < 10; ++i) to.act[i] = out->act[i];
+  for (int i = 0; i < 9; ++i) to.bits[i] = out->bits[i];
+  to.amax = out->amax;
+  to.ld = out->ld;
+  hipLaunchKernelGGL(mlp_x3_train_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                     as_stream(stream), (const float4*)w_slices, w_head, pts, dirs, zero, P,
+                     (float4*)raw, to);
+  return check_launch("mlp_x3_train_kernel");
+}
+
+extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_head, int64_t P,
+                                          int with_enc, const NerfX3BwdIO* io,
+                                          nerf_stream_t stream) {
+  NERF_REQUIRE(w_slices && w_head && io && io->d_raw && io->dmax,
+               "nerf_mlp_train_backward_x3: null pointer");
+  NERF_REQUIRE(P >= 0 && io->ld >= P, "nerf_mlp_train_backward_x3: bad size");
+  for (int i = 0; i < 10; ++i)
+    NERF_REQUIRE(io->d[i] != nullptr, "nerf_mlp_train_backward_x3: null output rows");
+  if (with_enc)
+    NERF_REQUIRE(io->d[10] && io->d[11], "nerf_mlp_train_backward_x3: null encoding rows");
+  for (int i = 0; i < 9; ++i)
+    NERF_REQUIRE(io->bits[i] != nullptr, "nerf_mlp_train_backward_x3: null relu bits");
+  NERF_REQUIRE((int64_t)256 * io->ld * 4 < (1ll << 31),
+               "nerf_mlp_train_backward_x3: rows too long for 32-bit offsets");
+  NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
+                   ((uintptr_t)io->d_raw & 15) == 0,
+               "nerf_mlp_train_backward_x3: weights/d_raw must be 16-byte aligned");
+  if (P == 0) return 0;
+  const int64_t blocks = cdiv(P, kX3Tile);
+  NERF_REQUIRE(blocks < (1ll << 31), "nerf_mlp_train_backward_x3: too many samples");
+  const int n_cu = stream_cu_count(stream);
+  const int64_t grid = blocks < n_cu ? blocks : n_cu;
+  X3BwdIO b;
+  b.d_raw = (const float4*)io->d_raw;
+  for (int i = 0; i < 9; ++i) b.bits[i] = io->bits[i];
+  for (int i = 0; i < 12; ++i) b.d[i] = io->d[i];
+  b.dmax = io->dmax;
+  b.ld = io->ld;
+  if (with_enc)
+    hipLaunchKernelGGL(mlp_x3_bwd_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                       as_stream(stream), (const float4*)w_slices, w_head, P, b);
+  else
+    hipLaunchKernelGGL(mlp_x3_bwd_kernel<false>, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                       as_stream(stream), (const float4*)w_slices, w_head, P, b);
+  return check_launch("mlp_x3_bwd_kernel");
 }
 
 extern "C" int nerf_mlp_forward_x3_list(const float* w_slices, const float* w_head,

@@ -86,6 +86,15 @@ struct StepViews {
   static constexpr int bsel(int g) { return Q0 + (g >> 2); }
 };
 
+// 64-row slices (the encoding rows of the backward: 4 tiles) = four K steps
+// (operands Q0 .. Q0+3) x 2 tile pairs: groups 2k, 2k+1 = K step Q0+k.
+template <int Q0, bool F = false>
+struct StepEnc4 {
+  static constexpr bool first(int g) { return F && g < 2; }
+  static constexpr int tile(int g) { return 2 * (g & 1); }
+  static constexpr int bsel(int g) { return Q0 + (g >> 1); }
+};
+
 // ---------------------------------------------------------------------------
 // activations: scale, FP16 split, B operands
 // ---------------------------------------------------------------------------

@@ -27,6 +27,8 @@ SIGNATURES = {
     "nerf_mlp_forward": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
     "nerf_mlp_forward_x3": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
     "nerf_mlp_forward_x3_list": (_I, [_P, _P, _P, _P, _P, _I64, _I, _P, _P, _I64, _P, _S]),
+    "nerf_mlp_train_forward_x3": (_I, [_P, _P, _P, _P, _P, _I64, _P, _P, _S]),
+    "nerf_mlp_train_backward_x3": (_I, [_P, _P, _I64, _I, _P, _S]),
     "nerf_ert_segment": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _I, _I, _F, _P, _P, _P, _P, _S]),
     "nerf_x3_layer": (_I, [_P, _P, _I, _I, _P, _P, _I64, _P, _I64, _P, _P, _I, _P, _I64, _I64,
                            _P, _S]),

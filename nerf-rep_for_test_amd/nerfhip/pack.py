@@ -332,26 +332,31 @@ def fold_feature_into_views(Wf, bf, Wv, bv):
     return W.astype(np.float32), b.astype(np.float32)
 
 
-def pack_mlp_x3(params, prefix="model"):
+def pack_mlp_x3(params, prefix="model", fold=True):
     """Packed network for nerf_mlp_forward_x3: (slices float32[65*8192] holding
     FP16 fragment pairs, head float32[3200]). The feature layer is folded into
-    the views layer (fold_feature_into_views): 11 % fewer MACs per sample."""
+    the views layer (fold_feature_into_views): 11 % fewer MACs per sample.
+    fold=False: the 73-slice stream of nerf_mlp_train_forward_x3, which keeps
+    the feature layer (8 slices between layer 7 and the views layer; the head
+    then carries the feature bias and the unfolded views bias)."""
     def get(name):
         v = params[f"{prefix}.{name}"]
         v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
         return np.ascontiguousarray(v, np.float32)
 
     _, head = pack_mlp(params, prefix)          # biases and VALU heads: same layout
-    Wc, bc = fold_feature_into_views(get("feature_linear.weight"), get("feature_linear.bias"),
-                                     get("views_linears.0.weight"), get("views_linears.0.bias"))
-    head[H_BIAS_VIEWS:H_BIAS_VIEWS + 128] = _group_pack(bc, 8).reshape(-1)
-    head[H_BIAS + 8 * 256:H_BIAS + 9 * 256] = 0.0   # feature bias: folded
+    if fold:
+        Wc, bc = fold_feature_into_views(get("feature_linear.weight"), get("feature_linear.bias"),
+                                         get("views_linears.0.weight"),
+                                         get("views_linears.0.bias"))
+        head[H_BIAS_VIEWS:H_BIAS_VIEWS + 128] = _group_pack(bc, 8).reshape(-1)
+        head[H_BIAS + 8 * 256:H_BIAS + 9 * 256] = 0.0   # feature bias: folded
     slices = []
     for li, (name, kind, tiles) in enumerate(layer_plan()):
-        if name == "feature_linear":
+        if name == "feature_linear" and fold:
             head[H_SCALES + li] = 0
             continue
-        Wt = Wc if name == "views_linears.0" else get(name + ".weight")
+        Wt = Wc if (fold and name == "views_linears.0") else get(name + ".weight")
         sw = weight_exponent(Wt)
         head[H_SCALES + li] = sw
         cols = _x3_layer_cols(kind)
@@ -366,7 +371,7 @@ def pack_mlp_x3(params, prefix="model"):
                 for qq in range(min(2, fr.shape[0] - q0)):
                     blk[16 * qq:16 * qq + 16] = fr[q0 + qq].reshape(16, 64, 8)
                 slices.append(blk)
-    assert len(slices) == X3_SLICES, len(slices)
+    assert len(slices) == (X3_SLICES if fold else SLICES), len(slices)
     allh = np.stack(slices).reshape(-1)
     return np.ascontiguousarray(allh).view(np.float32).copy(), head
 

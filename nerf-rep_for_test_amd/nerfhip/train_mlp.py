@@ -78,12 +78,13 @@ class X3Packer:
     Entries: name -> (param, transposed, rowmap, colmap); the padded matrix's
     element (i, k) is param[rowmap[i]][colmap[k]] (param^T when transposed)."""
 
-    def __init__(self, device):
+    def __init__(self, device, forward=True, backward=True):
         self.device = torch.device(device)
+        self.forward = forward
+        self.backward = backward
         self.key = None
 
-    @staticmethod
-    def plan(p):
+    def plan(self, p):
         ar = lambda n: list(range(n))   # noqa: E731
         enc64 = ar(63) + [-1]
         plan = {"fwd0": ("pts_linears.0.weight", False, ar(256), enc64),
@@ -100,6 +101,10 @@ class X3Packer:
         for i in (1, 2, 3, 4, 6, 7):
             plan[f"fwd{i}"] = (f"pts_linears.{i}.weight", False, ar(256), ar(256))
             plan[f"bwd{i}"] = (f"pts_linears.{i}.weight", True, ar(256), ar(256))
+        if not self.forward:
+            plan = {k: v for k, v in plan.items() if not k.startswith("fwd")}
+        if not self.backward:
+            plan = {k: v for k, v in plan.items() if not k.startswith("bwd")}
         return plan
 
     def _build(self, p):
@@ -138,17 +143,215 @@ class X3Packer:
                 for i, (n, (o, mt, nk)) in enumerate(self.out.items())}
 
 
+class X3StreamPacker:
+    """The training forward's weight stream, packed on the device from the live
+    parameters every step: the 73 slices of nerf_mlp_train_forward_x3 (the
+    inference kernel's layout with the feature layer kept: byte-identical to
+    nerfhip.pack.pack_mlp_x3(fold=False)) by one nerf_x3_pack launch set (each
+    layer's matrix with the kernel's K permutation as its column map, written
+    straight into its slices), and the head block (lane-packed biases, the
+    alpha / rgb heads, the per-layer weight scales) by one gather from the
+    parameters through an index map made once by nerfhip.pack.pack_mlp."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.key = None
+
+    @staticmethod
+    def plan():
+        from .pack import _x3_layer_cols, layer_plan
+        out, off = [], 0
+        for name, kind, tiles in layer_plan():
+            cols = _x3_layer_cols(kind).reshape(-1)
+            out.append((name + ".weight", list(range(16 * tiles)), [int(c) for c in cols], off))
+            off += -(-16 * tiles * len(cols) // 8192)          # whole slices (views: 4.5 -> 5)
+        return out, off
+
+    def _build(self, p):
+        import numpy as np
+        from .pack import HEAD_FLOATS, H_SCALES, SLICE_FLOATS, pack_mlp
+        dev = self.device
+        plan, nsl = self.plan()
+        self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
+        self.sw = torch.zeros(len(plan), device=dev, dtype=torch.int32)
+        self.maps, recs = [], []
+        for n, (pname, rmap, cmap, off) in enumerate(plan):
+            W = p[pname]
+            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
+            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
+            self.maps += [rm, cm]
+            recs.append((W.data_ptr(), W.stride(0), W.stride(1), rm.data_ptr(), cm.data_ptr(),
+                         len(rmap), len(cmap), self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
+                         self.sw[n:n + 1].data_ptr()))
+        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
+                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
+                       ("sw", "<u8")])
+        self.table = torch.from_numpy(np.array(recs, dtype=dt).view(np.uint8).copy()).to(dev)
+        # head: which source element every head float is (pack_mlp on index-valued
+        # parameters); sources = HEAD_SRC parameters flattened, then the 10 scales
+        src_n = [sum(int(np.prod(p[k].shape)) for k in HEAD_SRC[:i]) for i in range(len(HEAD_SRC))]
+        fake = {}
+        for k, v in PARAM_SHAPES.items():
+            fake["model." + k] = np.zeros(v, np.float32)
+        for k, o in zip(HEAD_SRC, src_n):
+            shape = tuple(p[k].shape)
+            fake["model." + k] = (o + 1 + np.arange(int(np.prod(shape)))).reshape(shape).astype(np.float32)
+        _, head = pack_mlp(fake, "model")
+        nsrc = src_n[-1] + int(np.prod(p[HEAD_SRC[-1]].shape))
+        idx = np.rint(head).astype(np.int64) - 1              # -1: zero
+        idx[H_SCALES:H_SCALES + len(plan)] = nsrc + np.arange(len(plan))
+        assert idx.max() < nsrc + len(plan) and head.shape[0] == HEAD_FLOATS
+        keep = np.nonzero(idx >= 0)[0]
+        self.head_dst = torch.from_numpy(keep).to(dev)
+        self.head_src = torch.from_numpy(idx[keep]).to(dev)
+        self.head = torch.zeros(HEAD_FLOATS, device=dev, dtype=torch.float32)
+
+    def pack(self, p):
+        """p: parameter name (PARAM_NAMES) -> tensor. Returns (stream, head) on the device."""
+        key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
+        if key != self.key:
+            self._build(p)
+            self.key = key
+        call("nerf_x3_pack", ptr(self.table), len(self.maps) // 2, _lib.stream_of(self.device))
+        src = torch.cat([p[k].detach().reshape(-1) for k in HEAD_SRC] + [self.sw.float()])
+        self.head.index_copy_(0, self.head_dst, src.index_select(0, self.head_src))
+        return self.stream, self.head
+
+
+class X3BwdStreamPacker(X3StreamPacker):
+    """The backward chain's weight stream (nerf_mlp_train_backward_x3), packed on
+    the device every step: the transposed matrices in consumption order, each
+    with the register-resident K permutation (x3_cols_act) as its column map --
+    W_views[:, :256]^T (4 slices), W_feat^T, W_7^T, W_6^T (8 each), [the
+    encoding rows of W_5^T: 2 slices of 4 tiles x 4 K steps], the h4 rows of
+    W_5^T, W_4^T .. W_1^T (8 each), [W_0^T: 2 slices]; with_enc: 72 slices,
+    else 68 -- and its head: the lane-packed rgb and alpha weights at the
+    forward head's offsets, the 11 weight scales at 3100 + j (j = matrix in
+    that order, fixed whether or not the encoding rows are packed)."""
+
+    def __init__(self, device, with_enc=True):
+        super().__init__(device)
+        self.with_enc = bool(with_enc)
+
+    def plan(self):
+        from .pack import x3_cols_act
+        ar = lambda n: list(range(n))   # noqa: E731
+        act = [int(c) for c in x3_cols_act().reshape(-1)]
+        act4 = [int(c) for c in x3_cols_act(4).reshape(-1)]
+        enc = ar(63) + [-1]
+        mats = [("views_linears.0.weight", ar(256), act4), ("feature_linear.weight", ar(256), act),
+                ("pts_linears.7.weight", ar(256), act), ("pts_linears.6.weight", ar(256), act),
+                ("pts_linears.5.weight", enc, act),
+                ("pts_linears.5.weight", [63 + i for i in range(256)], act)]
+        mats += [(f"pts_linears.{i}.weight", ar(256), act) for i in (4, 3, 2, 1)]
+        mats += [("pts_linears.0.weight", enc, act)]
+        out, off = [], 0
+        for j, (name, rmap, cmap) in enumerate(mats):
+            if not self.with_enc and j in (4, 10):
+                out.append((name, rmap, cmap, None, j))
+                continue
+            out.append((name, rmap, cmap, off, j))
+            off += -(-len(rmap) * len(cmap) // 8192)
+        return out, off
+
+    def _build(self, p):
+        import numpy as np
+        from .pack import H_ALPHA_W, H_RGB_W, HEAD_FLOATS, SLICE_FLOATS, _group_pack
+        dev = self.device
+        plan, nsl = self.plan()
+        self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
+        self.sw = torch.zeros(11, device=dev, dtype=torch.int32)
+        self.maps, recs = [], []
+        for name, rmap, cmap, off, j in plan:
+            if off is None:
+                continue
+            W = p[name]
+            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
+            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
+            self.maps += [rm, cm]
+            # transposed: element (i, k) = W[cmap[k]][rmap[i]]
+            recs.append((W.data_ptr(), W.stride(1), W.stride(0), rm.data_ptr(), cm.data_ptr(),
+                         len(rmap), len(cmap), self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
+                         self.sw[j:j + 1].data_ptr()))
+        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
+                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
+                       ("sw", "<u8")])
+        self.table = torch.from_numpy(np.array(recs, dtype=dt).view(np.uint8).copy()).to(dev)
+        # head: rgb W [3][4][32] and alpha W [4][64] lane-packed (pack_mlp's layout),
+        # then the scales: src = cat(rgb W (384), alpha W (256), sw (11))
+        idx = np.full(HEAD_FLOATS, -1, np.int64)
+        rgb_idx = np.arange(384).reshape(3, 128)
+        for c in range(3):
+            idx[H_RGB_W + c * 128:H_RGB_W + c * 128 + 128] = _group_pack(rgb_idx[c], 8).reshape(-1)
+        idx[H_ALPHA_W:H_ALPHA_W + 256] = 384 + _group_pack(np.arange(256), 16).reshape(-1)
+        idx[3100:3111] = 640 + np.arange(11)
+        keep = np.nonzero(idx >= 0)[0]
+        self.head_dst = torch.from_numpy(keep).to(dev)
+        self.head_src = torch.from_numpy(idx[keep]).to(dev)
+        self.head = torch.zeros(HEAD_FLOATS, device=dev, dtype=torch.float32)
+
+    def pack(self, p):
+        key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
+        if key != self.key:
+            self._build(p)
+            self.key = key
+        call("nerf_x3_pack", ptr(self.table), len(self.maps) // 2, _lib.stream_of(self.device))
+        src = torch.cat([p["rgb_linear.weight"].detach().reshape(-1),
+                         p["alpha_linear.weight"].detach().reshape(-1), self.sw.float()])
+        self.head.index_copy_(0, self.head_dst, src.index_select(0, self.head_src))
+        return self.stream, self.head
+
+
+class _BwdIO(ctypes.Structure):
+    """NerfX3BwdIO (include/nerfhip.h)."""
+    _fields_ = [("d_raw", ctypes.c_void_p), ("bits", ctypes.c_void_p * 9),
+                ("d", ctypes.c_void_p * 12), ("dmax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
+
+
+_BWD_STREAMS = {}
+
+
+def _bwd_stream_for(params, device, with_enc):
+    p = dict(zip(PARAM_NAMES, params))
+    key = (p["pts_linears.0.weight"].data_ptr(), bool(with_enc))
+    pk = _BWD_STREAMS.get(key)
+    if pk is None:
+        pk = _BWD_STREAMS[key] = X3BwdStreamPacker(device, with_enc)
+    return pk.pack(p)
+
+
+class _TrainOut(ctypes.Structure):
+    """NerfX3TrainOut (include/nerfhip.h)."""
+    _fields_ = [("act", ctypes.c_void_p * 10), ("bits", ctypes.c_void_p * 9),
+                ("amax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
+
+
 _PACKERS = {}
+_STREAMS = {}
+_ZERO = {}
 
 
-def _packs_for(params, device):
-    """Packed matrices of the network whose weight tensors these are (one packer
-    per network, keyed by the first weight's storage)."""
+def _stream_for(params, device):
+    """(stream, head) of the network whose parameters these are (one packer per
+    network, keyed by the first weight's storage)."""
     p = dict(zip(PARAM_NAMES, params))
     key = p["pts_linears.0.weight"].data_ptr()
+    pk = _STREAMS.get(key)
+    if pk is None:
+        pk = _STREAMS[key] = X3StreamPacker(device)
+    return pk.pack(p)
+
+
+def _packs_for(params, device, forward=True, backward=True):
+    """Packed matrices of the network whose weight tensors these are (one packer
+    per network and direction set, keyed by the first weight's storage);
+    forward=False / backward=False: without that direction's matrices (the fused
+    kernels stream their own)."""
+    p = dict(zip(PARAM_NAMES, params))
+    key = (p["pts_linears.0.weight"].data_ptr(), forward, backward)
     pk = _PACKERS.get(key)
     if pk is None:
-        pk = _PACKERS[key] = X3Packer(device)
+        pk = _PACKERS[key] = X3Packer(device, forward=forward, backward=backward)
     return pk.pack(p)
 
 
@@ -294,7 +497,27 @@ PARAM_NAMES = ([f"pts_linears.{i}.{k}" for i in range(8) for k in ("weight", "bi
                ["alpha_linear.weight", "alpha_linear.bias", "feature_linear.weight",
                 "feature_linear.bias", "views_linears.0.weight", "views_linears.0.bias",
                 "rgb_linear.weight", "rgb_linear.bias"])
+# shapes of one NeRF's parameters (network.py:9-47) and the head's sources
+PARAM_SHAPES = {**{f"pts_linears.{i}.weight": (256, 63 if i == 0 else 319 if i == 5 else 256)
+                   for i in range(8)},
+                **{f"pts_linears.{i}.bias": (256,) for i in range(8)},
+                "alpha_linear.weight": (1, 256), "alpha_linear.bias": (1,),
+                "feature_linear.weight": (256, 256), "feature_linear.bias": (256,),
+                "views_linears.0.weight": (128, 283), "views_linears.0.bias": (128,),
+                "rgb_linear.weight": (3, 128), "rgb_linear.bias": (3,)}
+HEAD_SRC = ([f"pts_linears.{i}.bias" for i in range(8)] +
+            ["feature_linear.bias", "views_linears.0.bias", "alpha_linear.weight",
+             "alpha_linear.bias", "rgb_linear.weight", "rgb_linear.bias"])
 
+
+# The forward as one fused launch (nerf_mlp_train_forward_x3) instead of ten
+# layer launches, the backward's chain of products likewise
+# (nerf_mlp_train_backward_x3); NERF_TRAIN_FUSED_FORWARD=0 /
+# NERF_TRAIN_FUSED_BACKWARD=0 select the layer launches (the parity tests run
+# both).
+import os as _os
+FUSED_FORWARD = _os.environ.get("NERF_TRAIN_FUSED_FORWARD", "1") != "0"
+FUSED_BACKWARD = _os.environ.get("NERF_TRAIN_FUSED_BACKWARD", "1") != "0"
 
 # Row padding of the feature-major activations: a row stride of P + 32 floats
 # (not P, a multiple of 2^13 at the C3 sizes) spreads the rows' same-sample
@@ -338,7 +561,12 @@ class NerfMLPFn(torch.autograd.Function):
         H = [_act(256, P, dev) if i not in (4,) else None
              for i in range(8)]
         H[4] = E[64:320]
-        pk = _packs_for(params, dev)
+        fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
+        pk = None if fused_f and fused_b else \
+            _packs_for(params, dev, forward=not fused_f, backward=not fused_b)
+        ctx.fused_backward = fused_b
+        if fused_f:
+            return NerfMLPFn._forward_fused(ctx, pts, pts_c, dirs, params, E, H, amax, pk)
         src = E[0:64]
         # the ReLU masks of h0..h7 as bits for the dgrad launches (32 B per sample
         # and layer instead of re-reading the 1 KiB of FP32 activations)
@@ -371,6 +599,43 @@ class NerfMLPFn(torch.autograd.Function):
         return raw
 
     @staticmethod
+    def _forward_fused(ctx, pts, pts_c, dirs, params, E, H, amax, pk):
+        """The forward as ONE nerf_mlp_train_forward_x3 launch (the inference
+        kernel's per-tile body over the unfolded stream, writing every layer's
+        output rows, ReLU bits and max |.|): what the ten layer launches of the
+        unfused forward produce, and the backward reads."""
+        dev = pts.device
+        P = pts.shape[0]
+        stream, head = _stream_for(params, dev)
+        V = _act(288, P, dev)                                      # cat(feature, views enc)
+        V[283:].zero_()
+        dirs_c = dirs.detach().contiguous()
+        _encode(dirs_c, DIR_FREQS, V[256:283], amax[10:11])
+        HV = _act(128, P, dev)
+        bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
+        bits_v = torch.empty((relu_bits_words(P, 8),), device=dev, dtype=torch.int16)
+        raw = torch.empty((P, 4), device=dev, dtype=torch.float32)
+        zero = _ZERO.get(str(dev))
+        if zero is None:
+            zero = _ZERO[str(dev)] = torch.zeros(1, device=dev, dtype=torch.float32)
+        out = _TrainOut()
+        for i in range(8):
+            out.act[i] = H[i].data_ptr()
+            out.bits[i] = bits[i].data_ptr()
+        out.act[8] = V[0:256].data_ptr()
+        out.act[9] = HV.data_ptr()
+        out.bits[8] = bits_v.data_ptr()
+        out.amax = amax.data_ptr()
+        out.ld = H[0].stride(0)
+        assert all(t.stride(0) == out.ld for t in (E, V, HV)) and H[0].stride(1) == 1
+        call("nerf_mlp_train_forward_x3", ptr(stream), ptr(head), ptr(pts_c), ptr(dirs_c),
+             ptr(zero), P, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
+        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
+        ctx.pts_grad = pts.requires_grad
+        ctx.packs = pk
+        return raw
+
+    @staticmethod
     def backward(ctx, d_raw):
         pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, bits_v, *params = ctx.saved_tensors
         H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
@@ -390,57 +655,28 @@ class NerfMLPFn(torch.autograd.Function):
         post[wb.add(d_rgb, HV, amax_b=amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
         dmax = torch.zeros(11, device=dev, dtype=f32)   # max |d| of each layer-kernel output
-        # d hv = (W_rgb^T d_rgb) * (hv > 0): the views layer's ReLU bits
-        d_hv = _act(128, P, dev)
-        wrt, swrt, mt, nk = pk["bwd_rgb"]
-        _layer(wrt, swrt, mt, nk, DR, d_hv, P, mask_bits=bits_v, amax=dmax[10:11])
+        need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
+        if ctx.fused_backward:
+            d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(d_raw, params, bits, bits_v, dmax,
+                                                           need_enc)
+        else:
+            d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
+                                                            need_enc)
         post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[8:9], amax[10:11]),
                     with_bias=True)] = (
             "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
-        # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
-        wvt, swvt, mt, nk = pk["bwd_views"]
-        DF = _act(256, P, dev)
-        _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
         post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
             "feature_linear.weight", "feature_linear.bias", None)
         post[wb.add(d_sig, H[7], amax_b=amax[7:8], with_bias=True)] = (
             "alpha_linear.weight", "alpha_linear.bias", None)
-        # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
-        wft, swft, _, _ = pk["bwd_feat"]
-        D = _act(256, P, dev)
-        aw = p["alpha_linear.weight"].reshape(-1).contiguous()
-        dsig = d_sig.reshape(-1).contiguous()
-        _layer(wft, swft, 16, 8, DF, D, P, mask_bits=bits[7], ru=aw, rw=dsig, amax=dmax[7:8])
-        d_enc = None
         for i in range(7, -1, -1):
             inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
             in_max = (torch.maximum(amax[9:10], amax[4:5]) if i == 5 else
                       amax[9:10] if i == 0 else amax[i - 1:i])
             fix = ((lambda g: g[:, :63]) if i == 0 else
                    (lambda g: torch.cat([g[:, :63], g[:, 64:320]], 1)) if i == 5 else None)
-            post[wb.add(D, inp, dmax[i:i + 1], in_max, with_bias=True)] = (
+            post[wb.add(D[i], inp, dmax[i:i + 1], in_max, with_bias=True)] = (
                 f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", fix)
-            need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
-            if i == 0:
-                if need_enc:
-                    wt, swt, mt, nk = pk["bwd0"]
-                    de = _act(64, P, dev)
-                    _layer(wt, swt, mt, nk, D, de, P)
-                    d_enc = de[:63] if d_enc is None else d_enc + de[:63]
-                break
-            Dn = _act(256, P, dev)
-            if i == 5:
-                wt, swt, mt, nk = pk["bwd5h"]
-                _layer(wt, swt, mt, nk, D, Dn, P, mask_bits=bits[4], amax=dmax[i - 1:i])
-                if need_enc:
-                    we, swe, mt, nk = pk["bwd5e"]
-                    de = _act(64, P, dev)
-                    _layer(we, swe, mt, nk, D, de, P)
-                    d_enc = de[:63]
-            else:
-                wt, swt, mt, nk = pk[f"bwd{i}"]
-                _layer(wt, swt, mt, nk, D, Dn, P, mask_bits=bits[i - 1], amax=dmax[i - 1:i])
-            D = Dn
         for slot, res in enumerate(wb.results()):
             wname, bname, fix = post[slot]
             gw, gb = (res if bname else (res, None))
@@ -453,6 +689,85 @@ class NerfMLPFn(torch.autograd.Function):
             call("nerf_freq_encode_fm_backward", ptr(d_enc), d_enc.stride(0), ptr(pts), 3, P,
                  XYZ_FREQS, ptr(d_pts), _lib.stream_of(dev))
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
+
+
+def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
+    """The backward's chain of products as layer launches: d hv, DF, D0..D7 and
+    (need_enc) the encoding gradient rows, dmax raised as the fused kernel does."""
+    dev = DR.device
+    P = DR.shape[1]
+    d_hv = _act(128, P, dev)   # d hv = (W_rgb^T d_rgb) * (hv > 0): the views layer's ReLU bits
+    wrt, swrt, mt, nk = pk["bwd_rgb"]
+    _layer(wrt, swrt, mt, nk, DR, d_hv, P, mask_bits=bits_v, amax=dmax[10:11])
+    # d feature = W_v[:, :256]^T d_hv (K = 128 -> 4 steps), no mask (no ReLU)
+    wvt, swvt, mt, nk = pk["bwd_views"]
+    DF = _act(256, P, dev)
+    _layer(wvt, swvt, mt, nk, d_hv, DF, P, amax=dmax[8:9])
+    # d h7 = (W_feat^T DF + W_alpha^T d_sig) * (h7 > 0)
+    wft, swft, _, _ = pk["bwd_feat"]
+    D = [None] * 8
+    D[7] = _act(256, P, dev)
+    aw = p["alpha_linear.weight"].reshape(-1).contiguous()
+    dsig = DR[3].contiguous()
+    _layer(wft, swft, 16, 8, DF, D[7], P, mask_bits=bits[7], ru=aw, rw=dsig, amax=dmax[7:8])
+    d_enc = None
+    for i in range(7, 0, -1):
+        D[i - 1] = _act(256, P, dev)
+        if i == 5:
+            wt, swt, mt, nk = pk["bwd5h"]
+            _layer(wt, swt, mt, nk, D[5], D[4], P, mask_bits=bits[4], amax=dmax[4:5])
+            if need_enc:
+                we, swe, mt, nk = pk["bwd5e"]
+                de = _act(64, P, dev)
+                _layer(we, swe, mt, nk, D[5], de, P)
+                d_enc = de[:63]
+        else:
+            wt, swt, mt, nk = pk[f"bwd{i}"]
+            _layer(wt, swt, mt, nk, D[i], D[i - 1], P, mask_bits=bits[i - 1],
+                   amax=dmax[i - 1:i])
+    if need_enc:
+        wt, swt, mt, nk = pk["bwd0"]
+        de = _act(64, P, dev)
+        _layer(wt, swt, mt, nk, D[0], de, P)
+        d_enc = de[:63] if d_enc is None else d_enc + de[:63]
+    return d_hv, DF, D, d_enc
+
+
+def _backward_fused_impl(d_raw, params, bits, bits_v, dmax, need_enc):
+    """The same chain as ONE nerf_mlp_train_backward_x3 launch over the
+    transposed weight stream (X3BwdStreamPacker): every product's rows written
+    feature-major and its max |.| raised, the ReLU masks from the forward's
+    bits; d_enc = the layer-5 and layer-0 encoding rows summed."""
+    dev = d_raw.device
+    P = d_raw.shape[0]
+    stream, head = _bwd_stream_for(params, dev, need_enc)
+    d_raw_c = d_raw.detach().to(torch.float32).contiguous()
+    if d_raw_c.data_ptr() % 16:
+        d_raw_c = d_raw_c.clone()
+    D = [_act(256, P, dev) for _ in range(8)]
+    DF, d_hv = _act(256, P, dev), _act(128, P, dev)
+    de5 = _act(64, P, dev) if need_enc else None
+    de0 = _act(64, P, dev) if need_enc else None
+    io = _BwdIO()
+    io.d_raw = d_raw_c.data_ptr()
+    for i in range(8):
+        io.bits[i] = bits[i].data_ptr()
+        io.d[i] = D[i].data_ptr()
+    io.bits[8] = bits_v.data_ptr()
+    io.d[8], io.d[9] = DF.data_ptr(), d_hv.data_ptr()
+    io.d[10] = de5.data_ptr() if need_enc else None
+    io.d[11] = de0.data_ptr() if need_enc else None
+    io.dmax = dmax.data_ptr()
+    io.ld = D[0].stride(0)
+    assert all(t.stride(0) == io.ld for t in [DF, d_hv] + ([de5, de0] if need_enc else []))
+    call("nerf_mlp_train_backward_x3", ptr(stream), ptr(head), P, int(bool(need_enc)),
+         ctypes.addressof(io), _lib.stream_of(dev))
+    d_enc = de5[:63] + de0[:63] if need_enc else None
+    return d_hv, DF, D, d_enc
+
+
+NerfMLPFn._backward_layers = staticmethod(_backward_layers_impl)
+NerfMLPFn._backward_fused = staticmethod(_backward_fused_impl)
 
 
 def mlp_params(model):

@@ -35,6 +35,14 @@ def _full_loss_tol(name, k):
     return max(2e-3, 2.0 * float(ts["gnorm_spread__" + k]))
 
 
+def _coarse_elem_tol(name, k):
+    """Per-element bound (x the tensor's norm) on a coarse-loss gradient: 1e-3,
+    or twice the reference's own relative L2 distance from itself under exact
+    reparametrisations when that is larger (tg_<name>.npz gcdist: up to 2.3e-3
+    on t2's gain-3 weights, where a ReLU unit at its edge flips)."""
+    return max(1e-3, 2.0 * float(load("tg_" + name)["gcdist__" + k]))
+
+
 def _elementwise_grads(name, grads, coarse=False):
     """Every element of every gradient tensor against the reference's
     (tests/golden/tg_<name>.npz, make_train_fullgrad.py): per tensor the relative
@@ -90,7 +98,8 @@ def test_forward_loss_and_gradients_match_reference(dev, mlp, ops):
         ref = float(z["gcnorm__" + k])
         g = p.grad.detach().double().cpu()
         assert abs(g.norm().item() - ref) <= 1e-3 * ref + 1e-12, k
-        assert np.abs(g.reshape(-1)[:64].numpy() - z["gchead__" + k]).max() <= 1e-3 * ref + 1e-12, k
+        assert np.abs(g.reshape(-1)[:64].numpy() - z["gchead__" + k]).max() <= \
+            _coarse_elem_tol("t1_train_step", k) * ref + 1e-12, k
     _elementwise_grads("t1_train_step", {k: p.grad for k, p in tr.named_parameters()},
                        coarse=True)
     # the full loss: the fine loss reaches the coarse net through the sample
@@ -207,7 +216,8 @@ def test_plugin_training_render_matches_reference(dev, name, mlp):
         ref = float(z["gcnorm__" + k])
         gk = p.grad.detach().double().cpu()
         assert abs(gk.norm().item() - ref) <= 1e-3 * ref + 1e-12, k
-        assert np.abs(gk.reshape(-1)[:64].numpy() - z["gchead__" + k]).max() <= 1e-3 * ref + 1e-12, k
+        assert np.abs(gk.reshape(-1)[:64].numpy() - z["gchead__" + k]).max() <= \
+            _coarse_elem_tol(name, k) * ref + 1e-12, k
     _elementwise_grads(name, {k: p.grad for k, p in params.items()}, coarse=True)
     net.zero_grad(set_to_none=True)
     (loss_c + loss_f).backward()

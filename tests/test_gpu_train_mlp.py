@@ -41,14 +41,38 @@ def _rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("P", [1000, 3000])
-def test_x3_train_mlp_forward_backward_match_torch(dev, P):
+def _relu_edge_samples(m, pts, dirs, tol=1e-6):
+    """Samples with a ReLU pre-activation within tol x the layer's max |.| of 0
+    in the reference module (network.py:49-74): there the ReLU decision is a
+    coin flip under any FP32 summation order (one such unit of one sample moves
+    that sample's gradients by O(1)), so gradient comparisons zero their d_raw."""
+    from nerfhip.train import freq_encode
+    with torch.no_grad():
+        x = torch.cat([freq_encode(pts, 10), freq_encode(dirs, 4)], -1)
+        p_in, v_in = x[:, :63], x[:, 63:]
+        h, edge = p_in, torch.zeros(pts.shape[0], dtype=torch.bool, device=pts.device)
+        for i, lin in enumerate(m.pts_linears):
+            pre = lin(h)
+            edge |= (pre.abs() <= tol * pre.abs().max()).any(1)
+            h = torch.relu(pre)
+            if i in m.skips:
+                h = torch.cat([p_in, h], -1)
+        pre = m.views_linears[0](torch.cat([m.feature_linear(h), v_in], -1))
+        edge |= (pre.abs() <= tol * pre.abs().max()).any(1)
+    return edge
+
+
+@pytest.mark.parametrize("P,fused", [(1000, True), (3000, True), (1000, False), (3000, False)])
+def test_x3_train_mlp_forward_backward_match_torch(dev, P, fused, monkeypatch):
+    from nerfhip import train_mlp
     from nerfhip.train import freq_encode
     from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    monkeypatch.setattr(train_mlp, "FUSED_FORWARD", fused)
     m = _model(dev)
     pts, dirs = _inputs(dev, P)
     g = torch.Generator(device=dev).manual_seed(2)
     d_raw = torch.randn((P, 4), device=dev, generator=g)
+    d_raw[_relu_edge_samples(m, pts, dirs)] = 0.0
 
     # reference: torch FP32 autograd of the reference module
     x = pts.clone().requires_grad_(True)
@@ -158,7 +182,7 @@ def test_x3_packer_matches_reference_packing(dev):
     p = dict(zip(PARAM_NAMES, mlp_params(m)))
     packer = X3Packer(dev)
     got = packer.pack(p)
-    for name, (pname, tr, rmap, cmap) in X3Packer.plan(p).items():
+    for name, (pname, tr, rmap, cmap) in packer.plan(p).items():
         W = p[pname].detach()
         W = W.t() if tr else W
         Wp = torch.zeros((len(rmap), len(cmap)), device=dev)
@@ -295,3 +319,143 @@ def test_x3_wgrad_batch_matches_matmul(dev):
             if bias:
                 rb = A.double().sum(1)
                 assert (gb.double() - rb).abs().max().item() / A.double().abs().sum(1).max().item() < 1e-6
+
+
+def test_x3_stream_packer_matches_host_packing(dev):
+    """X3StreamPacker (nerf_x3_pack into the 73-slice stream + the head gather)
+    == nerfhip.pack.pack_mlp_x3(fold=False): the stream bit for bit, the head
+    value for value (scales included)."""
+    from nerfhip.pack import pack_mlp_x3
+    from nerfhip.train_mlp import PARAM_NAMES, X3StreamPacker, mlp_params
+    m = _model(dev, seed=3, gain=2.5)
+    p = dict(zip(PARAM_NAMES, mlp_params(m)))
+    stream, head = X3StreamPacker(dev).pack(p)
+    ref_s, ref_h = pack_mlp_x3({"model." + k: v.detach().cpu() for k, v in p.items()}, fold=False)
+    assert torch.equal(stream.view(torch.int32).cpu(), torch.from_numpy(ref_s).view(torch.int32))
+    assert torch.equal(head.cpu(), torch.from_numpy(ref_h))
+
+
+@pytest.mark.parametrize("with_enc", [True, False])
+def test_x3_bwd_stream_packer_matches_host_packing(dev, with_enc):
+    """X3BwdStreamPacker: every transposed matrix's slices == pack_x3_matrix of
+    that matrix (rows / K columns through the plan's maps, -1 -> 0) bit for bit,
+    at the slice offsets the backward kernel consumes (72 / 68 slices); the
+    head's rgb / alpha weights where the forward head holds them, the scales at
+    3100 + matrix index."""
+    import numpy as np
+    from nerfhip.pack import H_ALPHA_W, H_RGB_W, SLICE_FLOATS, pack_mlp
+    from nerfhip.train_mlp import PARAM_NAMES, X3BwdStreamPacker, mlp_params, pack_x3_matrix
+    m = _model(dev, seed=3, gain=2.5)
+    p = dict(zip(PARAM_NAMES, mlp_params(m)))
+    pk = X3BwdStreamPacker(dev, with_enc)
+    stream, head = pk.pack(p)
+    plan, nsl = pk.plan()
+    assert nsl == (72 if with_enc else 68) and stream.numel() == nsl * SLICE_FLOATS
+    hd = head.cpu()
+    for name, rmap, cmap, off, j in plan:
+        if off is None:
+            continue
+        Wt = p[name].detach().t()
+        rm, cm = torch.tensor(rmap, device=dev), torch.tensor(cmap, device=dev)
+        T = torch.where((rm >= 0)[:, None] & (cm >= 0)[None, :],
+                        Wt[rm.clamp_min(0)][:, cm.clamp_min(0)], 0.0)   # +0.0, as the kernel
+        ref, sw = pack_x3_matrix(T.contiguous())
+        seg = stream[off * SLICE_FLOATS:off * SLICE_FLOATS + ref.numel()]
+        assert torch.equal(seg.view(torch.int32), ref.view(torch.int32)), name
+        assert int(hd[3100 + j]) == int(sw.item()), name
+    _, fwd_head = pack_mlp({"model." + k: v.detach().cpu() for k, v in p.items()})
+    for a, n in ((H_RGB_W, 384), (H_ALPHA_W, 256)):
+        assert np.array_equal(hd[a:a + n].numpy(), fwd_head[a:a + n])
+
+
+@pytest.mark.parametrize("P", [1, 130, 4096, 70001])
+def test_fused_train_forward_equals_layer_launches(dev, P, monkeypatch):
+    """nerf_mlp_train_forward_x3 (one launch) against the ten x3_layer_kernel
+    launches it replaces, on the same inputs: raw, every saved activation row
+    (h0..h7, feature, views output) and every max |.| within 1e-6 relative
+    (the same x3 arithmetic; the layer-0 and skip K steps run in another order),
+    the ReLU bits equal wherever the activation is not within 1e-6 of 0, and
+    the backward's gradients within 1e-5."""
+    from nerfhip import train_mlp
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    m = _model(dev, seed=4, gain=2.0)
+    pts, dirs = _inputs(dev, P, seed=5)
+    d_raw = torch.randn((P, 4), device=dev, generator=torch.Generator(device=dev).manual_seed(6))
+    d_raw[_relu_edge_samples(m, pts, dirs)] = 0.0
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(train_mlp, "FUSED_FORWARD", fused)
+        y = pts.clone().requires_grad_(True)
+        out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+        node = out.grad_fn
+        saved = [t.clone() for t in node.saved_tensors[:14]]
+        grads = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
+        res[fused] = (out.detach().clone(), saved, grads)
+    (o0, s0, g0), (o1, s1, g1) = res[False], res[True]
+    assert _rel(o1, o0) < 1e-6
+    # saved: pts, E, h0..h3, h5..h7, V, HV, amax, bits, bits_v
+    names = ["pts", "E", "h0", "h1", "h2", "h3", "h5", "h6", "h7", "V", "HV", "amax"]
+    for name, a, b in zip(names, s1[:12], s0[:12]):
+        assert a.shape == b.shape, name
+        assert _rel(a, b) < 1e-6, (name, _rel(a, b))
+    # ReLU bits (x3_layer_kernel's word layout, what the dgrad launches read):
+    # a bit can only differ where the activation sits at the ReLU's edge
+    for b0, b1, mt in ((s0[12], s1[12], 16), (s0[13], s1[13], 8)):
+        assert b0.shape == b1.shape
+        w = torch.arange(b0.shape[-1], device=dev)
+        lane, blk = w % 64, w // 64                   # word ((tile*8+wave)*mt/4 + k)*64 + lane
+        tw = blk // (mt // 4)
+        sample = (tw // 8) * 128 + (tw % 8) * 16 + lane % 16
+        valid = sample < P                             # words of samples past P are not written
+        assert float((b0 != b1)[..., valid].float().mean()) < 1e-3
+    for name, a, b in zip(["pts"] + PARAM_NAMES, g1, g0):
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("pts_grad", [True, False])
+@pytest.mark.parametrize("P", [1, 130, 4096, 70001])
+def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatch):
+    """nerf_mlp_train_backward_x3 (one launch) against the layer launches it
+    replaces, after the same forward: d hv, DF, D0..D7 and the encoding
+    gradient rows within 1e-5 of each tensor's max (d hv: FP32 on the VALU
+    instead of an x3 product over the 3 rgb rows; the rest the same x3
+    products), every max |.| slot within 1e-5, the same zeros (the forward's
+    ReLU bits), and the parameter / point gradients within 1e-5."""
+    from nerfhip import train_mlp
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    m = _model(dev, seed=7, gain=2.0)
+    pts, dirs = _inputs(dev, P, seed=8)
+    d_raw = torch.randn((P, 4), device=dev, generator=torch.Generator(device=dev).manual_seed(9))
+    rec = {}
+
+    def recording(key, fn, dmax_arg):
+        def w(*a):
+            out = fn(*a)
+            rows = [out[0], out[1], *out[2]] + ([out[3]] if out[3] is not None else [])
+            rec[key] = ([t.clone() for t in rows], a[dmax_arg].clone(), out[3] is None)
+            return out
+        return staticmethod(w)
+
+    monkeypatch.setattr(NerfMLPFn, "_backward_fused",
+                        recording(True, NerfMLPFn._backward_fused, 4))
+    monkeypatch.setattr(NerfMLPFn, "_backward_layers",
+                        recording(False, NerfMLPFn._backward_layers, 5))
+    grads = {}
+    for fused in (False, True):
+        monkeypatch.setattr(train_mlp, "FUSED_BACKWARD", fused)
+        y = pts.clone().requires_grad_(pts_grad)
+        out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+        wrt = ([y] if pts_grad else []) + mlp_params(m)
+        grads[fused] = torch.autograd.grad(out, wrt, d_raw)
+    (r0, m0, n0), (r1, m1, n1) = rec[False], rec[True]
+    assert n0 == n1 == (not pts_grad) and len(r0) == len(r1) == (11 if pts_grad else 10)
+    names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc"]
+    for name, a, b in zip(names, r1, r0):
+        assert a.shape == b.shape, name
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
+        if name not in ("DF", "d_enc"):   # masked products: the same zeros
+            assert float(((a == 0) != (b == 0)).float().mean()) <= 1e-6, name
+    slots = [0, 1, 2, 3, 4, 5, 6, 7, 8, 10]
+    assert torch.allclose(m1[slots], m0[slots], rtol=1e-5, atol=0), (m1, m0)
+    for name, a, b in zip((["pts"] if pts_grad else []) + PARAM_NAMES, grads[True], grads[False]):
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
