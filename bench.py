@@ -201,6 +201,8 @@ def main():
         roof = roofline(precision, timer, elapsed, world, H, W,
                         pmc_workload=world == 1 and not ess_ert)
         roof["byte_kernels"] = byte_kernels(stages, steps)
+        if precision == "f16x3" and not ess_ert:
+            roof.update(held_clock(pipe, H, W, roof["achieved"], roof["peak"]))
         return pipe, elapsed, roof
 
     pipe, elapsed, roof = measure(args.precision, c4, args.steps, args.warmup)
@@ -410,13 +412,54 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
     return result
 
 
+def held_clock(pipe, H, W, achieved, peak, reps=3):
+    """The shader clock the chip holds while mlp_x3_kernel runs, measured right
+    after the timed frames (chip warm, same weights, a frame's coarse pass:
+    800 x 800 rays x 64 depths) by the kernel's diagnostic twin
+    (nerf_mlp_forward_x3_clock: d s_memtime / d s_memrealtime x 100 MHz per
+    workgroup, median; MI355X_MICROARCH.md DVFS give-back item 6), and the
+    kernel's fraction of the dense FP16 MFMA peak at that clock (the nominal
+    peak is quoted at 2.4 GHz)."""
+    import torch
+    from nerfhip._lib import call, ptr, stream_of
+    dev = pipe.device
+    ro, rd = pipe.camera_rays(H, W, *lego_camera(H, W, 0))
+    n, S = ro.shape[0], 64
+    z = torch.linspace(2.0, 6.0, S, device=dev)
+    raw = torch.empty((n * S, 4), device=dev)
+    clk = torch.zeros(4 * 4096, device=dev, dtype=torch.int64)
+    trace = torch.zeros(512 * 4, device=dev, dtype=torch.int64)
+    ghz = []
+    for _ in range(reps):
+        clk.zero_()
+        trace.zero_()
+        call("nerf_mlp_forward_x3_clock", ptr(pipe.coarse[0]), ptr(pipe.coarse[1]), ptr(ro),
+             ptr(rd), ptr(z), 0, n, S, ptr(raw), ptr(clk), clk.numel(), ptr(trace),
+             stream_of(dev))
+        torch.cuda.synchronize()
+        c = clk.view(-1, 4).cpu().numpy().astype(np.float64)
+        c = c[c[:, 3] > c[:, 2]]
+        ghz.append(float(np.median((c[:, 1] - c[:, 0]) / (c[:, 3] - c[:, 2]) * 0.1)))
+    f = float(np.median(ghz))
+    # the tile-start share: sample loads + encoding before the first MFMA, of the
+    # tile's cycles (workgroups 0-3, their first 32 tiles, the last run)
+    t = trace.view(-1, 4).cpu().numpy().astype(np.float64)
+    t = t[(t[:, 2] > t[:, 0]) & (t[:, 1] >= t[:, 0])]
+    start = float(np.median((t[:, 1] - t[:, 0]) / (t[:, 2] - t[:, 0]))) if len(t) else None
+    return {"held_clock_ghz": f, "held_clock_runs_ghz": ghz,
+            "peak_at_held_clock": peak * f / 2.4, "frac_at_held_clock": achieved / (peak * f / 2.4),
+            "tile_start_share": start,
+            "tile_cycles": float(np.median(t[:, 2] - t[:, 0])) if len(t) else None}
+
+
 def train_roofline(mlp, flop, step_s):
     """C3: the whole step's algorithmic MLP FLOP/s (fwd + 2x bwd) against the MFMA
     peak of the arithmetic the MLP GEMMs run on (x3: 3 FP16 MFMA products per
     FP32 product; torch: FP32 hipBLASLt)."""
     algo = flop / step_s / 1e12
     if mlp == "x3":
-        kernel, achieved, peak, unit = ("whole step (x3_layer_kernel + x3_wgrad_kernel dominate)",
+        kernel, achieved, peak, unit = ("whole step (mlp_x3_train_kernel, mlp_x3_bwd_kernel and "
+                                        "x3_wgrad_batch_kernel dominate)",
                                         3 * algo, FP16_MFMA_PEAK_TFLOPS,
                                         "TFLOP/s (FP16 MFMA, 3 per FP32 product)")
     else:

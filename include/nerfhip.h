@@ -198,6 +198,12 @@ typedef struct NerfWgradDesc {
   int M, N;
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
+/* The same with a K split per output tile: tile_chunks[t] (1 .. zmax, < 256)
+ *   for the tiles in the order descriptor, N tile, M tile (256 x 256 tiles, at
+ *   most 40); subset c < tile_chunks[t] of tile t writes partial row c, rows
+ *   tile_chunks[t] .. zmax-1 of the tile (and of its bias rows) are zeros. */
+int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const int* tile_chunks, int zmax,
+                          nerf_stream_t stream);
 
 /* nerf_mlp_train_forward_x3: the whole forward of a training step's MLP in ONE
  *   launch (the inference kernel over the 73-slice stream that keeps the
@@ -207,13 +213,15 @@ int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stre
  *   raw[p] = (rgb logits, sigma) as nerf_mlp_forward_x3; besides, every
  *   output is written feature-major with row stride out->ld floats:
  *   act[L] = h_L (rows 0..255) for L = 0..7, act[8] = feature (256 rows),
- *   act[9] = the views layer's output (128 rows); bits[L] = the ReLU bits of
- *   h_L (nerf_x3_layer_ex's layout, m_tiles 16) for L = 0..7 and bits[8] those
- *   of the views output (m_tiles 8); amax[0..8], amax[11] (device floats,
+ *   act[9] = the views layer's output (128 rows), act[10] = the xyz encoding
+ *   (64 rows: freq.py's 63 columns, row 63 = 0), act[11] = the view encoding
+ *   (32 rows: 27 columns, rows 27..31 = 0); bits[L] = the ReLU bits of h_L
+ *   (nerf_x3_layer_ex's layout, m_tiles 16) for L = 0..7 and bits[8] those of
+ *   the views output (m_tiles 8); amax[0..11] (device floats,
  *   caller-initialised, >= 0) are raised to max |h_0..h_7|, max |feature|,
- *   max |views output| (slots 9, 10 untouched). */
+ *   max |xyz encoding|, max |view encoding|, max |views output|. */
 typedef struct NerfX3TrainOut {
-  float* act[10];
+  float* act[12];
   unsigned short* bits[9];
   float* amax;
   int64_t ld;
@@ -239,8 +247,25 @@ typedef struct NerfX3BwdIO {
   float* dmax;
   int64_t ld;
 } NerfX3BwdIO;
+/* nerf_mlp_forward_x3_clock: nerf_mlp_forward_x3's computation (same outputs)
+ *   by a diagnostic twin of its kernel that stamps (s_memtime, s_memrealtime)
+ *   around each workgroup's work: clk[4 b + 0..3] = (memtime start, end,
+ *   realtime start, end) of workgroup b (clk 32-byte aligned, clk_len >= 4 x
+ *   workgroups; entries past the launched workgroups are left as they were).
+ *   The held shader clock = d memtime / d realtime x 100 MHz. trace (512 x 4
+ *   u64): workgroups 0..3 stamp memtime at each of their first 32 tiles'
+ *   start, after its sample loads + encoding, and at its end:
+ *   trace[(b * 32 + i) * 4 + 0..2]. */
+int nerf_mlp_forward_x3_clock(const float* w_slices, const float* w_head, const float* rays_o,
+                              const float* rays_d, const float* z, int64_t z_stride, int64_t n,
+                              int S, float* raw, unsigned long long* clk, int64_t clk_len,
+                              unsigned long long* trace, nerf_stream_t stream);
 int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_head, int64_t P,
                                int with_enc, const NerfX3BwdIO* io, nerf_stream_t stream);
+/* nerf_raw_absmax: amax[0] / amax[1] (caller-initialised, >= 0) raised to
+ *   max |raw[p][0..2]| / max |raw[p][3]| over p < P (the rgb / alpha heads'
+ *   weight-gradient scales from d_raw [P][4], 16-byte aligned). */
+int nerf_raw_absmax(const float* raw, int64_t P, float* amax, nerf_stream_t stream);
 /* nerf_freq_encode_fm: the frequency encoding of freq.py:7-32 (reference
  *   embed_fn / embeddirs_fn, encoding/__init__.py:7-18), written feature-major
  *   for the training MLP: out[j * ldo + p] for the 3 + 6 * n_freq columns of
@@ -253,12 +278,21 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
  *   feature-major [3 + 6 * n_freq][ldd]. */
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream);
-/* nerf_x3_pack: packs n weight matrices for nerf_x3_layer in one launch. descs
- * (device) = n records {const float* src; int64_t ldr, ldc; const int* rowmap;
- * const int* colmap; int M, K; void* out; int* sw} (64 bytes each): padded
- * element (i, k) = src[rowmap[i]*ldr + colmap[k]*ldc] (0 where a map entry is
- * -1); out receives the FP16 (hi, lo) fragments, *sw the scale exponent. */
-int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream);
+/* The same on d_enc + d_enc2 (elementwise, same row stride): the encoding's
+ * two consumers' gradients summed in the kernel. */
+int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
+                                     const float* x, int64_t ldx, int64_t P, int n_freq,
+                                     float* dx, nerf_stream_t stream);
+/* nerf_x3_pack: packs n weight matrices for the x3 training kernels in one
+ * launch set. descs (device) = n records {const float* src; int64_t ldr, ldc;
+ * const int* rowmap; const int* colmap; int M, K; void* out; int* sw;
+ * unsigned* amax} (72 bytes each): padded element (i, k) = src[rowmap[i]*ldr +
+ * colmap[k]*ldc] (0 where a map entry is -1); out receives the FP16 (hi, lo)
+ * fragments, *sw the scale exponent; *amax must be 0 on entry and is 0 again
+ * on exit. heads (device) = n_heads records {const uint64_t* table; float* dst;
+ * int64_t n}: dst[i] = the float at address table[i], or (bit 0 set) the scale
+ * exponent of the matrix whose amax slot is table[i] - 1, or 0 (table[i] 0). */
+int nerf_x3_pack(const void* descs, int n, const void* heads, int n_heads, nerf_stream_t stream);
 
 /* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
  * Reductions follow torch's CPU float32 summation order.

@@ -48,10 +48,15 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 // The fragment register sets, live across slices (x: even groups, y: odd),
 // and the stream length (a compile-time constant of each kernel: 65 slices for
 // inference, where the feature layer is folded into the views layer, 73 for
-// the training forward, which keeps it).
+// the training forward, which keeps it, 72 / 68 for the backward). The
+// backward without the encoding products reads the 72-slice stream minus its
+// encoding slices: logical slice t >= gap is stored at t + 2 (the last two
+// are never reached; nphys slices in memory).
 struct FragPipe {
   Frags x, y;
   int ns;
+  int gap = 1 << 20;
+  int nphys = 0;
 };
 
 // The weight stream runs three slices ahead of the compute.
@@ -123,9 +128,11 @@ __device__ __forceinline__ void run_slice3(Acc& acc, const Ring& R, int g, const
   const int t = g + kX3DmaAhead;
   // the stream runs on into the next tile (the last tile's wrapped pieces are
   // staged but never read): every slice stages one, every slice_end counts 2
-  const int ts = t < fp.ns ? t : t - fp.ns;
+  int ts = t < fp.ns ? t : t - fp.ns;
+  ts += ts >= fp.gap ? 2 : 0;
   run_group3<0, NG, Cfg, NEXT>(acc, base, lds_base(R.buf(g + 1), R.lane), bv, fp,
-                               x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane, fp.ns), hook);
+                               x3_dma(R.slices, ts, R.buf(t), R.wave, R.lane,
+                                      fp.nphys ? fp.nphys : fp.ns), hook);
 }
 
 // End of slice g: this wave's LDS-DMA of slice g+2 has landed (the next
@@ -385,11 +392,28 @@ struct ActStore {
 
 // Output locations of the training forward (nerf_mlp_train_forward_x3).
 struct X3TrainOut {
-  float* act[10];               // h0..h7, feature, views-layer output (rows, stride ld)
+  float* act[12];               // h0..h7, feature, views-layer output, the xyz encoding (64
+                                // rows, 63 = 0), the view encoding (32 rows, 27.. = 0); stride ld
   unsigned short* bits[9];      // ReLU bits of h0..h7 (x3_layer_kernel MT 16) and views (MT 8)
-  float* amax;                  // [12]: raised to max |.| of h0..h7 (0-7), feature (8), views (11)
+  float* amax;                  // [12]: raised to max |.| of h0..h7 (0-7), feature (8), xyz
+                                // encoding (9), view encoding (10), views (11)
   int64_t ld;                   // row stride of every output, floats
 };
+
+// Encoding rows of the training forward: the feature index (freq.py's column
+// order) of slot (q, j) of lane group g in encode_xyz's register layout
+// (x3_cols_enc), 63 for its one padding slot; encode_dir's (x3_cols_dir), 27..31
+// for its padding slots. Every row 0..63 / 0..31 is written exactly once.
+__device__ __forceinline__ int enc_xyz_row(int g, int q, int j) {
+  const int t = 4 * q + (j >> 1), pr = 8 * g + t;
+  if (pr < 30) return ((j & 1) ? 6 : 3) + 6 * (pr / 3) + pr % 3;
+  return t == 6 ? (j & 1) : ((j & 1) ? 63 : 2);
+}
+__device__ __forceinline__ int enc_dir_row(int g, int j) {
+  if (j < 6) return ((j & 1) ? 6 : 3) + 6 * g + (j >> 1);
+  if (j == 6) return g < 3 ? g : 27;
+  return 28 + g;
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, int64_t ld) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)((int64_t)rows * ld * 4), 0x00020000);
@@ -399,13 +423,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, 
 // written by the ERT segment kernel; the count is read on the device, so a
 // segmented evaluation needs no host round trip); raw is written at those
 // indices. Otherwise the samples are 0 .. total.
-template <bool LIST, bool TRAIN>
+// TRACE (diagnostic twin only): the first lane of workgroups 0..3 stamps
+// s_memtime at each of its first 32 tiles' start, after the tile's sample
+// loads + encoding, and at its end: trace[(b * 32 + i) * 4 + 0..2].
+template <bool LIST, bool TRAIN, bool TRACE = false>
 __device__ __forceinline__ void mlp_x3_body(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
     float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count,
-    const X3TrainOut& to) {
+    const X3TrainOut& to, unsigned long long* trace = nullptr) {
   if constexpr (LIST) total = *count;
   __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
   __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
@@ -433,6 +460,12 @@ __device__ __forceinline__ void mlp_x3_body(
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const bool first_tile = tile == (int64_t)blockIdx.x;
   const int64_t gs = tile * kX3Tile + wave * 16 + (lane & 15);
+  const int ti = (int)((tile - blockIdx.x) / gridDim.x);
+  const bool tr = TRACE && blockIdx.x < 4 && ti < 32 && threadIdx.x == 0;
+  unsigned long long* trp = TRACE ? trace + ((int64_t)blockIdx.x * 32 + ti) * 4 : nullptr;
+  if constexpr (TRACE) {
+    if (tr) trp[0] = __builtin_amdgcn_s_memtime();
+  }
   // recomputed per tile: otherwise the encoding's per-lane constants are
   // hoisted out of the tile loop and, live through every slice, spill
   int g4 = lane >> 4;
@@ -452,6 +485,23 @@ __device__ __forceinline__ void mlp_x3_body(
   Op encf[2];                   // FP32 encoding (split in place for the skip layer)
   encode_xyz(p, g4, encf);
   const float enc_max = sample_max(fmaxf(op_absmax(encf[0]), op_absmax(encf[1])));
+  if constexpr (TRACE) {
+    asm volatile("" ::"v"(enc_max));
+    if (tr) trp[1] = __builtin_amdgcn_s_memtime();
+  }
+  if constexpr (TRAIN) {   // the encoding rows (the wgrad operand of layers 0 and 5)
+    int i10 = 10;
+    asm volatile("" : "+s"(i10));
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i10], 64, to.ld);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned vo = valid ? (unsigned)(((int64_t)enc_xyz_row(g4, q, j) * to.ld + gs) * 4)
+                                  : 0x7fffffffu;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(encf[q][j]), rs, (int)vo, 0, 0);
+      }
+  }
 
   using Epi = EpiHook;   // (the training stores ride on the next slices' hooks)
   using Pend = typename std::conditional<TRAIN, ActStore, NoPend>::type;
@@ -507,6 +557,7 @@ __device__ __forceinline__ void mlp_x3_body(
     slice256<1>(acc, R, 1, E, fp, epi);
     epi.finish(acc);
     amax_to_lds(0, epi.amax);
+    amax_to_lds(9, enc_max);
     e = act_exponent(sample_max(epi.amax));
   }
   // TRAIN: h0 goes to HBM pair by pair in the next layer's slices (pair 0 now)
@@ -575,6 +626,18 @@ __device__ __forceinline__ void mlp_x3_body(
   // inference: feature = W_f h7 + b_f folded in (W_views,feat W_f on h7) ---------
   Op dirf;
   encode_dir(dv, g4, dirf);
+  if constexpr (TRAIN) {   // the view-encoding rows (the views layer's wgrad operand)
+    int i11 = 11;
+    asm volatile("" : "+s"(i11));
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i11], 32, to.ld);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned vo = valid ? (unsigned)(((int64_t)enc_dir_row(g4, j) * to.ld + gs) * 4)
+                                : 0x7fffffffu;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dirf[j]), rs, (int)vo, 0, 0);
+    }
+    amax_to_lds(10, op_absmax(dirf));
+  }
   {
     float mx = op_absmax(dirf);
 #pragma unroll
@@ -646,6 +709,9 @@ __device__ __forceinline__ void mlp_x3_body(
 #pragma unroll
   for (int c = 0; c < 3; ++c) rgb[c] = quad_sum(part[c]) + hd[kHeadRgbB + c];
   if (valid && g4 == 0) raw[gc] = make_float4(rgb[0], rgb[1], rgb[2], alpha);
+  if constexpr (TRACE) {
+    if (tr) trp[2] = __builtin_amdgcn_s_memtime();
+  }
   R.rot = (R.rot + kNs) & 3;   // the next tile's slice 0 = this stream's slice kNs
   }
   // the last tile's wrapped DMA pieces land before the workgroup's LDS is freed
@@ -668,6 +734,31 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_kernel(
     float4* __restrict__ raw, const int* __restrict__ list, const int* __restrict__ count) {
   mlp_x3_body<LIST, false>(slices, head, rays_o, rays_d, z, z_stride, total, S, raw, list, count,
                            X3TrainOut{});
+}
+
+// Diagnostic twin of mlp_x3_kernel<false> (nerf_mlp_forward_x3_clock): the same
+// body between two stamps of (s_memtime, s_memrealtime) per workgroup, written
+// by its first lane to clk[4 b ..]: the shader clock the chip held during the
+// launch is d memtime / d memrealtime x 100 MHz (MI355X_MICROARCH.md, DVFS
+// give-back item 6). The production kernel carries no stamp.
+__global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_clock_kernel(
+    const float4* __restrict__ slices, const float* __restrict__ head,
+    const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+    const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
+    float4* __restrict__ raw, unsigned long long* __restrict__ clk,
+    unsigned long long* __restrict__ trace) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  mlp_x3_body<false, false, true>(slices, head, rays_o, rays_d, z, z_stride, total, S, raw,
+                                  nullptr, nullptr, X3TrainOut{}, trace);
+  __syncthreads();
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    ulonglong4 v;
+    v.x = t0; v.y = t1; v.z = r0; v.w = r1;
+    reinterpret_cast<ulonglong4*>(clk)[blockIdx.x] = v;
+  }
 }
 
 // The training forward: samples p = 0 .. P-1 at pts[p] with view direction
@@ -696,7 +787,8 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_train_kernel(
 // masks are the forward's bits, loaded one slice before the epilogue that
 // applies them. Stream (pack: nerfhip.train_mlp.X3BwdStreamPacker): W_views^T
 // (4), W_feat^T (8), W_7^T, W_6^T (8 each), [W_5,enc^T (2)], W_5,h^T, W_4^T ..
-// W_1^T (8 each), [W_0^T (2)]: 72 slices with ENC, 68 without.
+// W_1^T (8 each), W_0^T (2): 72 slices (without ENC the 4 encoding slices are
+// skipped).
 // ===========================================================================
 constexpr int kBwdScales = 3100;   // per-matrix weight scale exponents [11] in the head
 
@@ -856,13 +948,15 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   Ring R{ring, slices, wave, lane};
   constexpr int kNs = ENC ? 72 : 68;
   for (int t = 0; t < kX3DmaAhead; ++t)   // all 8 waves, 4 pieces each
-    stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, kNs));
+    stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, 72));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
   if (tid < 11) dmax_lds[tid] = 0u;
 
   FragPipe fp;
   fp.ns = kNs;
+  fp.nphys = 72;
+  if (!ENC) fp.gap = 28;   // the encoding slices 28, 29 skipped (70, 71: past the end)
   const int64_t ntiles = (P + kX3Tile - 1) / kX3Tile;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const bool first_tile = tile == (int64_t)blockIdx.x;
@@ -1675,27 +1769,47 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
 }
 
 // Several weight gradients in one launch (the whole backward of a network):
-// workgroup w -> (descriptor, output tile, K subset z of Z) with the Z subsets
-// of a tile adjacent, so every layer is split Z ways instead of ~256 and its
-// partials are Z x M x N instead of 256 x M x N (nerf_x3_wgrad_batch).
+// workgroup w -> (output tile t, K subset z of Z_t), the subsets of a tile
+// adjacent. Z_t is per tile (nerf_x3_wgrad_batch_z): a tile whose operand rows
+// are few (the heads, the 32- / 64-row remainders) streams fewer bytes per K
+// step, so it takes fewer workgroups for the same finish time and the full
+// tiles more. Partials: Zmax x M x N per descriptor; a tile's rows z >= Z_t
+// are written as zeros (by its z = 0 workgroup) so one fixed-order sum over
+// Zmax rows serves every tile.
 constexpr int kWgBatchMax = 16;
+constexpr int kWgTilesMax = 40;
 struct WgradBatch {
   NerfWgradDesc d[kWgBatchMax];
-  int tiles_end[kWgBatchMax];   // prefix sums of mtiles * ntiles
-  int n, Z;
+  unsigned char t_desc[kWgTilesMax], t_m[kWgTilesMax], t_n[kWgTilesMax], t_z[kWgTilesMax];
+  int t_wg_end[kWgTilesMax];   // prefix sums of Z_t
+  int nt, Zmax;
 };
 
 __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const WgradBatch bt) {
   __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
-  const int z = (int)(blockIdx.x % (unsigned)bt.Z);
-  int tile = (int)(blockIdx.x / (unsigned)bt.Z);
-  int k = 0;
-  while (k + 1 < bt.n && tile >= bt.tiles_end[k]) ++k;
-  if (k > 0) tile -= bt.tiles_end[k - 1];
-  const NerfWgradDesc& d = bt.d[k];
-  const int mt = (d.M + kWgTile - 1) / kWgTile;
+  const int w = (int)blockIdx.x;
+  int t = 0;
+  while (t + 1 < bt.nt && w >= bt.t_wg_end[t]) ++t;
+  const int Z = bt.t_z[t];
+  const int z = w - (bt.t_wg_end[t] - Z);
+  const NerfWgradDesc& d = bt.d[bt.t_desc[t]];
+  const int mtile = bt.t_m[t], ntile = bt.t_n[t];
   wgrad_dma_body(stg, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, d.amax_a, d.amax_b, d.part,
-                 d.ldpart, d.bias_part, d.ldbias, tile % mt, tile / mt, z, bt.Z);
+                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z);
+  if (z != 0 || Z >= bt.Zmax) return;
+  // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)
+  const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
+  const int rows = min(kWgTile, d.M - m0), cols = min(kWgTile, d.N - n0);
+  for (int zz = Z; zz < bt.Zmax; ++zz) {
+    float* out = d.part + (int64_t)zz * d.ldpart;
+    for (int i = threadIdx.x; i < rows * cols; i += kTrainThreads) {
+      const int m = m0 + i / cols, n = n0 + i % cols;
+      out[(int64_t)m * d.N + n] = 0.0f;
+    }
+    if (d.bias_part && ntile == 0)
+      for (int i = threadIdx.x; i < rows; i += kTrainThreads)
+        d.bias_part[(int64_t)zz * d.ldbias + m0 + i] = 0.0f;
+  }
 }
 
 
@@ -1712,18 +1826,24 @@ struct X3PackDesc {
   int M, K;
   uint4* out;
   int* sw;
+  unsigned* amax;   // max |W| as float bits: 0 on entry, reset to 0 by the last launch
+};
+
+// A head block gathered in the packing launch: dst[i] = *(float*)table[i], or
+// the scale exponent of the matrix whose amax slot table[i] & ~1 is (bit 0
+// set), or 0 (table[i] == 0).
+struct X3HeadGather {
+  const uint64_t* table;
+  float* dst;
+  int64_t n;
 };
 
 // Packing in three launches over (matrix, slab) blocks: the max |W| of every
-// matrix accumulated as float bits into its sw slot (zeroed first), the scale
-// exponent derived from it by every packing block, and the slot rewritten
-// with the exponent by a last one-thread-per-matrix launch.
+// matrix accumulated as float bits into its amax slot, then every packing
+// block derives the scale exponent from it (and the head blocks are gathered),
+// then a one-thread-per-matrix launch writes the exponent into sw and resets
+// the amax slot for the next packing.
 constexpr int kPackSlabs = 16;   // blocks per matrix
-
-__global__ void x3_pack_zero_kernel(const X3PackDesc* __restrict__ descs, int n) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < n) *descs[m].sw = 0;
-}
 
 __global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __restrict__ descs) {
   const X3PackDesc d = descs[blockIdx.x];
@@ -1737,7 +1857,7 @@ __global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __r
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
   if ((threadIdx.x & 63) == 0)   // values >= 0: the float bits order like the floats
-    atomicMax(reinterpret_cast<unsigned*>(d.sw), __float_as_uint(mx));
+    atomicMax(d.amax, __float_as_uint(mx));
 }
 
 __device__ __forceinline__ int pack_exponent(float amax) {
@@ -1746,9 +1866,23 @@ __device__ __forceinline__ int pack_exponent(float amax) {
   return amax > 0.0f ? 12 - E : 0;   // max |W| 2^sw in [2^11, 2^12)
 }
 
-__global__ __launch_bounds__(256) void x3_pack_kernel(const X3PackDesc* __restrict__ descs) {
+__global__ __launch_bounds__(256) void x3_pack_kernel(const X3PackDesc* __restrict__ descs, int n,
+                                                     const X3HeadGather* __restrict__ heads) {
+  if ((int)blockIdx.x >= n) {   // a head block's slab
+    const X3HeadGather h = heads[blockIdx.x - n];
+    const int64_t per = (h.n + kPackSlabs - 1) / kPackSlabs;
+    const int64_t i0 = blockIdx.y * per, i1 = min(h.n, i0 + per);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+      const uint64_t e = h.table[i];
+      float v = 0.0f;
+      if (e & 1u) v = (float)pack_exponent(__uint_as_float(*reinterpret_cast<const unsigned*>(e - 1u)));
+      else if (e) v = *reinterpret_cast<const float*>(e);
+      h.dst[i] = v;
+    }
+    return;
+  }
   const X3PackDesc d = descs[blockIdx.x];
-  const float amax = __uint_as_float(*reinterpret_cast<const unsigned*>(d.sw));
+  const float amax = __uint_as_float(*d.amax);
   const float scale = ldexpf(1.0f, pack_exponent(amax));
   const int mt = d.M / 16;
   const int groups = (d.K / 32) * mt * 64;   // (q, t, lane) -> 8 halfs hi + 8 halfs lo
@@ -1776,7 +1910,10 @@ __global__ __launch_bounds__(256) void x3_pack_kernel(const X3PackDesc* __restri
 
 __global__ void x3_pack_scale_kernel(const X3PackDesc* __restrict__ descs, int n) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m < n) *descs[m].sw = pack_exponent(__uint_as_float(*reinterpret_cast<unsigned*>(descs[m].sw)));
+  if (m < n) {
+    *descs[m].sw = pack_exponent(__uint_as_float(*descs[m].amax));
+    *descs[m].amax = 0u;
+  }
 }
 
 }  // namespace nerfhip
@@ -1805,6 +1942,27 @@ extern "C" int nerf_mlp_forward_x3(const float* w_slices, const float* w_head, c
   return check_launch("mlp_x3_kernel");
 }
 
+extern "C" int nerf_mlp_forward_x3_clock(const float* w_slices, const float* w_head,
+                                         const float* rays_o, const float* rays_d, const float* z,
+                                         int64_t z_stride, int64_t n, int S, float* raw,
+                                         unsigned long long* clk, int64_t clk_len,
+                                         unsigned long long* trace, nerf_stream_t stream) {
+  NERF_REQUIRE(w_slices && w_head && rays_o && rays_d && z && raw && clk && trace,
+               "nerf_mlp_forward_x3_clock: null pointer");
+  NERF_REQUIRE(n > 0 && S >= 1 && z_stride >= 0, "nerf_mlp_forward_x3_clock: bad size");
+  NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
+                   ((uintptr_t)raw & 15) == 0 && ((uintptr_t)clk & 31) == 0,
+               "nerf_mlp_forward_x3_clock: weights/raw/clk misaligned");
+  const int64_t blocks = cdiv(n * S, kX3Tile);
+  const int n_cu = stream_cu_count(stream);
+  const int64_t grid = blocks < n_cu ? blocks : n_cu;
+  NERF_REQUIRE(clk_len >= 4 * grid, "nerf_mlp_forward_x3_clock: clk holds < 4 per workgroup");
+  hipLaunchKernelGGL(mlp_x3_clock_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                     as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
+                     z_stride, n * S, S, (float4*)raw, clk, trace);
+  return check_launch("mlp_x3_clock_kernel");
+}
+
 extern "C" int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_head,
                                          const float* pts, const float* dirs, const float* zero,
                                          int64_t P, const NerfX3TrainOut* out, float* raw,
@@ -1812,7 +1970,7 @@ extern "C" int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_h
   NERF_REQUIRE(w_slices && w_head && pts && dirs && zero && out && raw && out->amax,
                "nerf_mlp_train_forward_x3: null pointer");
   NERF_REQUIRE(P >= 0 && out->ld >= P, "nerf_mlp_train_forward_x3: bad size");
-  for (int i = 0; i < 10; ++i)
+  for (int i = 0; i < 12; ++i)
     NERF_REQUIRE(out->act[i] != nullptr, "nerf_mlp_train_forward_x3: null output rows");
   for (int i = 0; i < 9; ++i)
     NERF_REQUIRE(out->bits[i] != nullptr, "nerf_mlp_train_forward_x3: null relu bits");
@@ -1827,7 +1985,7 @@ extern "C" int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_h
   const int n_cu = stream_cu_count(stream);
   const int64_t grid = blocks < n_cu ? blocks : n_cu;
   X3TrainOut to;
-  for (int i = 0; i < 10; ++i) to.act[i] = out->act[i];
+  for (int i = 0; i < 12; ++i) to.act[i] = out->act[i];
   for (int i = 0; i < 9; ++i) to.bits[i] = out->bits[i];
   to.amax = out->amax;
   to.ld = out->ld;
@@ -2008,12 +2166,12 @@ extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B,
 }
 
 
-extern "C" int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks,
-                                   nerf_stream_t stream) {
-  NERF_REQUIRE(descs && n >= 1 && n <= kWgBatchMax && chunks >= 1 && chunks < 65536,
+extern "C" int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const int* tile_chunks,
+                                     int zmax, nerf_stream_t stream) {
+  NERF_REQUIRE(descs && tile_chunks && n >= 1 && n <= kWgBatchMax && zmax >= 1 && zmax < 65536,
                "nerf_x3_wgrad_batch: bad arguments");
   WgradBatch bt;
-  int64_t tiles = 0;
+  int nt = 0, wgs = 0;
   for (int k = 0; k < n; ++k) {
     const NerfWgradDesc& d = descs[k];
     NERF_REQUIRE(d.A && d.B && d.amax_a && d.amax_b && d.part && d.M > 0 && d.N > 0 &&
@@ -2023,27 +2181,47 @@ extern "C" int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks
     NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P),
                  "nerf_x3_wgrad_batch: operands must be aligned (P % 32 == 0, 16-B rows, < 2 GiB)");
     bt.d[k] = d;
-    tiles += (int64_t)cdiv(d.M, kWgTile) * cdiv(d.N, kWgTile);
-    bt.tiles_end[k] = (int)tiles;
+    const int mt = (int)cdiv(d.M, kWgTile), ntl = (int)cdiv(d.N, kWgTile);
+    for (int j = 0; j < ntl; ++j)       // tile order: descriptor, then N tile, then M tile
+      for (int i = 0; i < mt; ++i) {
+        NERF_REQUIRE(nt < kWgTilesMax, "nerf_x3_wgrad_batch: too many tiles");
+        const int Z = tile_chunks[nt];
+        NERF_REQUIRE(Z >= 1 && Z <= zmax && Z < 256, "nerf_x3_wgrad_batch: bad tile chunks");
+        bt.t_desc[nt] = (unsigned char)k;
+        bt.t_m[nt] = (unsigned char)i;
+        bt.t_n[nt] = (unsigned char)j;
+        bt.t_z[nt] = (unsigned char)Z;
+        wgs += Z;
+        bt.t_wg_end[nt] = wgs;
+        ++nt;
+      }
   }
-  bt.n = n;
-  bt.Z = chunks;
-  NERF_REQUIRE(tiles * chunks < (1ll << 31), "nerf_x3_wgrad_batch: too many workgroups");
-  hipLaunchKernelGGL(x3_wgrad_batch_kernel, dim3((unsigned)(tiles * chunks)), dim3(kTrainThreads),
-                     0, as_stream(stream), bt);
+  bt.nt = nt;
+  bt.Zmax = zmax;
+  hipLaunchKernelGGL(x3_wgrad_batch_kernel, dim3((unsigned)wgs), dim3(kTrainThreads), 0,
+                     as_stream(stream), bt);
   return check_launch("x3_wgrad_batch_kernel");
 }
 
-extern "C" int nerf_x3_pack(const void* descs, int n, nerf_stream_t stream) {
-  NERF_REQUIRE(descs && n >= 0 && n < 65536, "nerf_x3_pack: bad arguments");
-  if (n == 0) return 0;
+extern "C" int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks,
+                                   nerf_stream_t stream) {
+  NERF_REQUIRE(descs && n >= 1 && n <= kWgBatchMax && chunks >= 1 && chunks < 256,
+               "nerf_x3_wgrad_batch: bad arguments");
+  int zs[kWgTilesMax];
+  for (int i = 0; i < kWgTilesMax; ++i) zs[i] = chunks;
+  return nerf_x3_wgrad_batch_z(descs, n, zs, chunks, stream);
+}
+
+extern "C" int nerf_x3_pack(const void* descs, int n, const void* heads, int n_heads,
+                            nerf_stream_t stream) {
+  NERF_REQUIRE(descs && n > 0 && n < 65536 && n_heads >= 0 && n_heads < 256 &&
+                   (heads || n_heads == 0),
+               "nerf_x3_pack: bad arguments");
   const X3PackDesc* d = (const X3PackDesc*)descs;
-  hipLaunchKernelGGL(x3_pack_zero_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64), 0,
-                     as_stream(stream), d, n);
   hipLaunchKernelGGL(x3_pack_amax_kernel, dim3((unsigned)n, kPackSlabs), dim3(256), 0,
                      as_stream(stream), d);
-  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)n, kPackSlabs), dim3(256), 0,
-                     as_stream(stream), d);
+  hipLaunchKernelGGL(x3_pack_kernel, dim3((unsigned)(n + n_heads), kPackSlabs), dim3(256), 0,
+                     as_stream(stream), d, n, (const X3HeadGather*)heads);
   hipLaunchKernelGGL(x3_pack_scale_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64), 0,
                      as_stream(stream), d, n);
   return check_launch("x3_pack_kernel");

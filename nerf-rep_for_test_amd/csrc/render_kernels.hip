@@ -770,29 +770,74 @@ __global__ __launch_bounds__(64 * kEncMaxWaves) void freq_encode_fm_kernel(
 
 // d x_c = d_enc[c] + sum_f 2^f (cos(2^f x_c) d_sin - sin(2^f x_c) d_cos): the
 // chain rule through the encoding (autograd of freq.py's cat of sin/cos).
+// With d_enc2, d_enc = d_enc + d_enc2 elementwise first (the encoding feeds two
+// layers: autograd's sum of their input gradients).
 __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
-    const float* __restrict__ d_enc, int64_t ldd, const float* __restrict__ x, int64_t ldx,
-    int64_t P, int L, float* __restrict__ dx) {
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
+    const float* __restrict__ x, int64_t ldx, int64_t P, int L, float* __restrict__ dx) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
+  auto de = [&](int row) {
+    float v = d_enc[row * ldd + p];
+    if (d_enc2) v = v + d_enc2[row * ldd + p];
+    return v;
+  };
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float v = x[p * ldx + c];
-    float g = d_enc[c * ldd + p];
+    float g = de(c);
     for (int f = 0; f < L; ++f) {
       const float k = (float)(1 << f);
       const float a = v * k;
       float sn, cs;
       sincosf(a, &sn, &cs);
-      const float ds = d_enc[(3 + 6 * f + c) * ldd + p] * cs -
-                       d_enc[(6 + 6 * f + c) * ldd + p] * sn;
+      const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
       g = g + ds * k;
     }
     dx[p * 3 + c] = g;
   }
 }
 
+// max |rgb| / |sigma| of raw [P][4] (float bits: the values are >= 0)
+__global__ __launch_bounds__(256) void raw_absmax_kernel(const float4* __restrict__ raw, int64_t P,
+                                                         unsigned* __restrict__ amax) {
+  float mr = 0.0f, ms = 0.0f;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < P; p += (int64_t)gridDim.x * 256) {
+    const float4 v = raw[p];
+    mr = fmaxf(mr, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)));
+    ms = fmaxf(ms, fabsf(v.w));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mr = fmaxf(mr, __shfl_xor(mr, o));
+    ms = fmaxf(ms, __shfl_xor(ms, o));
+  }
+  __shared__ float part[2][4];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wave] = mr;
+    part[1][wave] = ms;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {   // one atomic per workgroup and value
+    const float m = fmaxf(fmaxf(part[threadIdx.x][0], part[threadIdx.x][1]),
+                          fmaxf(part[threadIdx.x][2], part[threadIdx.x][3]));
+    atomicMax(amax + threadIdx.x, __float_as_uint(m));
+  }
+}
+
 extern "C" {
+int nerf_raw_absmax(const float* raw, int64_t P, float* amax, nerf_stream_t stream) {
+  NERF_REQUIRE(raw && amax && P >= 0, "nerf_raw_absmax: bad arguments");
+  NERF_REQUIRE(((uintptr_t)raw & 15) == 0, "nerf_raw_absmax: raw must be 16-byte aligned");
+  if (P == 0) return 0;
+  // 4 float4 per thread at least: a few hundred atomics per launch, not thousands
+  const int64_t blocks = cdiv(P, 1024) < 256 ? cdiv(P, 1024) : 256;
+  hipLaunchKernelGGL(raw_absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     (const float4*)raw, P, (unsigned*)amax);
+  return check_launch("raw_absmax_kernel");
+}
+
 int nerf_ert_segment(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
                      int64_t n, int S, int s0, int s1, int s2, float thr, double* T,
                      unsigned char* active, int* list, int* count, nerf_stream_t stream) {
@@ -941,12 +986,18 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
 
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream) {
+  return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, x, ldx, P, n_freq, dx, stream);
+}
+
+int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
+                                     const float* x, int64_t ldx, int64_t P, int n_freq,
+                                     float* dx, nerf_stream_t stream) {
   NERF_REQUIRE(d_enc && x && dx, "nerf_freq_encode_fm_backward: null pointer");
   NERF_REQUIRE(P >= 0 && ldx >= 3 && ldd >= P && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm_backward: bad size");
   if (P == 0) return 0;
   hipLaunchKernelGGL(freq_encode_fm_backward_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
-                     as_stream(stream), d_enc, ldd, x, ldx, P, n_freq, dx);
+                     as_stream(stream), d_enc, d_enc2, ldd, x, ldx, P, n_freq, dx);
   return check_launch("freq_encode_fm_backward_kernel");
 }
 

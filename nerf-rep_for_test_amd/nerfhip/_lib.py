@@ -26,6 +26,7 @@ SIGNATURES = {
     "nerf_sample_coarse": (_I, [_P, _P, _I64, _I, _P, _S]),
     "nerf_mlp_forward": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
     "nerf_mlp_forward_x3": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
+    "nerf_mlp_forward_x3_clock": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _P, _I64, _P, _S]),
     "nerf_mlp_forward_x3_list": (_I, [_P, _P, _P, _P, _P, _I64, _I, _P, _P, _I64, _P, _S]),
     "nerf_mlp_train_forward_x3": (_I, [_P, _P, _P, _P, _P, _I64, _P, _P, _S]),
     "nerf_mlp_train_backward_x3": (_I, [_P, _P, _I64, _I, _P, _S]),
@@ -36,14 +37,17 @@ SIGNATURES = {
                               _I64, _P, _P, _P, _P, _P, _I, _P, _I, _S]),
     "nerf_sum_partials": (_I, [_P, _I64, _I64, _P, _S]),
     "nerf_x3_wgrad_batch": (_I, [_P, _I, _I, _S]),
+    "nerf_x3_wgrad_batch_z": (_I, [_P, _I, _P, _I, _S]),
     "nerf_x3_wgrad": (_I, [_P, _I64, _I, _P, _I64, _I, _I64, _I64, _P, _P, _P, _P, _S]),
-    "nerf_x3_pack": (_I, [_P, _I, _S]),
+    "nerf_x3_pack": (_I, [_P, _I, _P, _I, _S]),
     "nerf_composite_train_fwd": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _S]),
     "nerf_composite_train_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _P, _P, _P, _P,
                                       _P, _P, _P, _S]),
     "nerf_sample_pdf_bwd": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _S]),
     "nerf_freq_encode_fm": (_I, [_P, _I64, _I64, _I, _P, _I64, _P, _S]),
     "nerf_freq_encode_fm_backward": (_I, [_P, _I64, _P, _I64, _I64, _I, _P, _S]),
+    "nerf_raw_absmax": (_I, [_P, _I64, _P, _S]),
+    "nerf_freq_encode_fm_backward_sum": (_I, [_P, _P, _I64, _P, _I64, _I64, _I, _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_sample_fine": (_I, [_P, _I64, _P, _P, _I64, _I64, _I, _I, _P, _S]),

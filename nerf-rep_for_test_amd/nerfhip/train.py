@@ -369,6 +369,9 @@ class NerfTrainer:
     def _step_eager(self, rays_o, rays_d, target, t_rand=None, u=None, group=None):
         t_rand, u = self._draws(rays_o.shape[0], t_rand, u)
         self.opt.zero_grad(set_to_none=True)
+        if self.mlp == "x3":   # both networks' weight streams in one packing launch set
+            from .train_mlp import prepack
+            prepack([self.coarse] + ([self.fine] if self.N_importance > 0 else []))
         losses = self.loss(self.forward(rays_o, rays_d, t_rand, u), target)
         losses["loss"].backward()
         if group is not None:   # parameters without a gradient (e.g. no fine pass) skipped

@@ -25,6 +25,7 @@ ops, no host sync): packing order = ``pack_x3_matrix``.
 from __future__ import annotations
 
 import ctypes
+import os as _os
 
 import torch
 
@@ -68,10 +69,60 @@ def pack_x3_matrix(W):
     return fr.view(torch.float32).reshape(-1), sw
 
 
-class X3Packer:
+_DESC_FIELDS = [("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
+                ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"), ("sw", "<u8"),
+                ("amax", "<u8")]
+_HEAD_FIELDS = [("table", "<u8"), ("dst", "<u8"), ("n", "<i8")]
+
+
+def _device_table(recs, fields, device):
+    """Records (tuples) -> the packed C structs as a uint8 device tensor."""
+    import numpy as np
+    dt = np.dtype(fields)
+    arr = np.array(recs, dtype=dt)
+    return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+class _PackSet:
+    """Packing descriptors (X3PackDesc records: matrix -> fragments) and head
+    gathers (X3HeadGather records) of one or more streams; run as ONE
+    nerf_x3_pack launch set (amax, pack + gather, scale)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.key = None
+        self.recs, self.heads = [], []
+        self._keep = []
+
+    def _matrix(self, W, rmap, cmap, transposed, out_ptr, sw_ptr, amax_ptr):
+        dev = self.device
+        rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
+        cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
+        self._keep += [rm, cm]
+        ldr, ldc = (W.stride(1), W.stride(0)) if transposed else (W.stride(0), W.stride(1))
+        self.recs.append((W.data_ptr(), ldr, ldc, rm.data_ptr(), cm.data_ptr(), len(rmap),
+                          len(cmap), out_ptr, sw_ptr, amax_ptr))
+
+    def _head(self, table, dst):
+        """table: numpy uint64 [n] (addresses / scale slots | 1 / 0) -> gathered into dst."""
+        t = torch.from_numpy(table.astype("<u8").view("<i8")).to(self.device)
+        self._keep.append(t)
+        self.heads.append((t.data_ptr(), dst.data_ptr(), int(table.shape[0])))
+
+    def launch(self):
+        if not hasattr(self, "_tables") or self._tables[0] is None:
+            self._tables = (_device_table(self.recs, _DESC_FIELDS, self.device),
+                            _device_table(self.heads, _HEAD_FIELDS, self.device)
+                            if self.heads else None)
+        descs, heads = self._tables
+        call("nerf_x3_pack", ptr(descs), len(self.recs), ptr(heads), len(self.heads),
+             _lib.stream_of(self.device))
+
+
+class X3Packer(_PackSet):
     """All 21 weight matrices of one network's training step (forward W and
     backward W^T, padded as the layer kernels need them) packed by ONE
-    nerf_x3_pack launch from the live parameters; the output buffers, index
+    nerf_x3_pack launch set from the live parameters; the output buffers, index
     maps and descriptor table are built once and reused while the parameters
     keep their storage (the optimizer updates them in place).
 
@@ -79,10 +130,9 @@ class X3Packer:
     element (i, k) is param[rowmap[i]][colmap[k]] (param^T when transposed)."""
 
     def __init__(self, device, forward=True, backward=True):
-        self.device = torch.device(device)
+        super().__init__(device)
         self.forward = forward
         self.backward = backward
-        self.key = None
 
     def plan(self, p):
         ar = lambda n: list(range(n))   # noqa: E731
@@ -108,29 +158,19 @@ class X3Packer:
         return plan
 
     def _build(self, p):
-        import numpy as np
         plan = self.plan(p)
         dev = self.device
+        self.recs, self.heads, self._keep, self._tables = [], [], [], (None, None)
         self.names = list(plan)
-        self.out, self.maps, recs = {}, [], []
+        self.out = {}
         self.sw = torch.zeros(len(plan), device=dev, dtype=torch.int32)
+        self.amax = torch.zeros(len(plan), device=dev, dtype=torch.int32)
         for n, (pname, tr, rmap, cmap) in enumerate(plan.values()):
-            W = p[pname]
             M, K = len(rmap), len(cmap)
-            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
-            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
-            self.maps += [rm, cm]
             out = torch.empty(M * K, device=dev, dtype=torch.float32)   # M*K halfs x 2
             self.out[self.names[n]] = (out, M // 16, K // 32)
-            ldr, ldc = (W.stride(0), W.stride(1)) if not tr else (W.stride(1), W.stride(0))
-            recs.append((W.data_ptr(), ldr, ldc, rm.data_ptr(), cm.data_ptr(), M, K,
-                         out.data_ptr(), self.sw[n:n + 1].data_ptr()))
-        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
-                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
-                       ("sw", "<u8")])
-        assert dt.itemsize == 64
-        table = np.array(recs, dtype=dt)
-        self.table = torch.from_numpy(table.view(np.uint8).copy()).to(dev)
+            self._matrix(p[pname], rmap, cmap, tr, out.data_ptr(), self.sw[n:n + 1].data_ptr(),
+                         self.amax[n:n + 1].data_ptr())
 
     def pack(self, p):
         """p: parameter name -> tensor. Returns name -> (packed, sw [1], m_tiles, k_steps)."""
@@ -138,24 +178,37 @@ class X3Packer:
         if key != self.key:
             self._build(p)
             self.key = key
-        call("nerf_x3_pack", ptr(self.table), len(self.names), _lib.stream_of(self.device))
+        self.launch()
         return {n: (o, self.sw[i:i + 1], mt, nk)
                 for i, (n, (o, mt, nk)) in enumerate(self.out.items())}
 
 
-class X3StreamPacker:
-    """The training forward's weight stream, packed on the device from the live
-    parameters every step: the 73 slices of nerf_mlp_train_forward_x3 (the
-    inference kernel's layout with the feature layer kept: byte-identical to
-    nerfhip.pack.pack_mlp_x3(fold=False)) by one nerf_x3_pack launch set (each
-    layer's matrix with the kernel's K permutation as its column map, written
-    straight into its slices), and the head block (lane-packed biases, the
-    alpha / rgb heads, the per-layer weight scales) by one gather from the
-    parameters through an index map made once by nerfhip.pack.pack_mlp."""
+def _src_pointers(p, names, idx, amax, nsrc):
+    """Head gather table: index map over cat(names' parameters flattened, scales)
+    -> element addresses (scales: their amax slot | 1; -1: 0)."""
+    import numpy as np
+    sizes = [p[k].numel() for k in names]
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    assert starts[-1] == nsrc and all(p[k].is_contiguous() for k in names)
+    bases = np.array([p[k].data_ptr() for k in names], dtype=np.uint64)
+    out = np.zeros(idx.shape[0], np.uint64)
+    src = (idx >= 0) & (idx < nsrc)
+    k = np.searchsorted(starts, idx[src], side="right") - 1
+    out[src] = bases[k] + 4 * (idx[src] - starts[k]).astype(np.uint64)
+    sc = idx >= nsrc
+    out[sc] = np.uint64(amax.data_ptr()) + 4 * (idx[sc] - nsrc).astype(np.uint64) + np.uint64(1)
+    return out
 
-    def __init__(self, device):
-        self.device = torch.device(device)
-        self.key = None
+
+class X3StreamPacker(_PackSet):
+    """The training forward's weight stream, packed on the device from the live
+    parameters: the 73 slices of nerf_mlp_train_forward_x3 (the inference
+    kernel's layout with the feature layer kept: byte-identical to
+    nerfhip.pack.pack_mlp_x3(fold=False)), each layer's matrix with the kernel's
+    K permutation as its column map, written straight into its slices, and the
+    head block (lane-packed biases, the alpha / rgb heads, the per-layer weight
+    scales) gathered from the parameters through an index map made once by
+    nerfhip.pack.pack_mlp -- all in the nerf_x3_pack launch set."""
 
     @staticmethod
     def plan():
@@ -172,21 +225,14 @@ class X3StreamPacker:
         from .pack import HEAD_FLOATS, H_SCALES, SLICE_FLOATS, pack_mlp
         dev = self.device
         plan, nsl = self.plan()
+        self.recs, self.heads, self._keep, self._tables = [], [], [], (None, None)
         self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
         self.sw = torch.zeros(len(plan), device=dev, dtype=torch.int32)
-        self.maps, recs = [], []
+        self.amax = torch.zeros(len(plan), device=dev, dtype=torch.int32)
         for n, (pname, rmap, cmap, off) in enumerate(plan):
-            W = p[pname]
-            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
-            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
-            self.maps += [rm, cm]
-            recs.append((W.data_ptr(), W.stride(0), W.stride(1), rm.data_ptr(), cm.data_ptr(),
-                         len(rmap), len(cmap), self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
-                         self.sw[n:n + 1].data_ptr()))
-        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
-                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
-                       ("sw", "<u8")])
-        self.table = torch.from_numpy(np.array(recs, dtype=dt).view(np.uint8).copy()).to(dev)
+            self._matrix(p[pname], rmap, cmap, False,
+                         self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
+                         self.sw[n:n + 1].data_ptr(), self.amax[n:n + 1].data_ptr())
         # head: which source element every head float is (pack_mlp on index-valued
         # parameters); sources = HEAD_SRC parameters flattened, then the 10 scales
         src_n = [sum(int(np.prod(p[k].shape)) for k in HEAD_SRC[:i]) for i in range(len(HEAD_SRC))]
@@ -201,10 +247,8 @@ class X3StreamPacker:
         idx = np.rint(head).astype(np.int64) - 1              # -1: zero
         idx[H_SCALES:H_SCALES + len(plan)] = nsrc + np.arange(len(plan))
         assert idx.max() < nsrc + len(plan) and head.shape[0] == HEAD_FLOATS
-        keep = np.nonzero(idx >= 0)[0]
-        self.head_dst = torch.from_numpy(keep).to(dev)
-        self.head_src = torch.from_numpy(idx[keep]).to(dev)
         self.head = torch.zeros(HEAD_FLOATS, device=dev, dtype=torch.float32)
+        self._head(_src_pointers(p, HEAD_SRC, idx, self.amax, nsrc), self.head)
 
     def pack(self, p):
         """p: parameter name (PARAM_NAMES) -> tensor. Returns (stream, head) on the device."""
@@ -212,28 +256,23 @@ class X3StreamPacker:
         if key != self.key:
             self._build(p)
             self.key = key
-        call("nerf_x3_pack", ptr(self.table), len(self.maps) // 2, _lib.stream_of(self.device))
-        src = torch.cat([p[k].detach().reshape(-1) for k in HEAD_SRC] + [self.sw.float()])
-        self.head.index_copy_(0, self.head_dst, src.index_select(0, self.head_src))
+        self.launch()
         return self.stream, self.head
 
 
-class X3BwdStreamPacker(X3StreamPacker):
+class X3BwdStreamPacker(_PackSet):
     """The backward chain's weight stream (nerf_mlp_train_backward_x3), packed on
-    the device every step: the transposed matrices in consumption order, each
-    with the register-resident K permutation (x3_cols_act) as its column map --
-    W_views[:, :256]^T (4 slices), W_feat^T, W_7^T, W_6^T (8 each), [the
-    encoding rows of W_5^T: 2 slices of 4 tiles x 4 K steps], the h4 rows of
-    W_5^T, W_4^T .. W_1^T (8 each), [W_0^T: 2 slices]; with_enc: 72 slices,
-    else 68 -- and its head: the lane-packed rgb and alpha weights at the
-    forward head's offsets, the 11 weight scales at 3100 + j (j = matrix in
-    that order, fixed whether or not the encoding rows are packed)."""
+    the device: the transposed matrices in consumption order, each with the
+    register-resident K permutation (x3_cols_act) as its column map --
+    W_views[:, :256]^T (4 slices), W_feat^T, W_7^T, W_6^T (8 each), the
+    encoding rows of W_5^T (2 slices of 4 tiles x 4 K steps), the h4 rows of
+    W_5^T, W_4^T .. W_1^T (8 each), W_0^T (2 slices): 72 slices (the kernel
+    without the encoding products skips slices 28, 29, 70, 71) -- and its head:
+    the lane-packed rgb and alpha weights at the forward head's offsets, the 11
+    weight scales at 3100 + j (j = matrix in that order)."""
 
-    def __init__(self, device, with_enc=True):
-        super().__init__(device)
-        self.with_enc = bool(with_enc)
-
-    def plan(self):
+    @staticmethod
+    def plan():
         from .pack import x3_cols_act
         ar = lambda n: list(range(n))   # noqa: E731
         act = [int(c) for c in x3_cols_act().reshape(-1)]
@@ -247,9 +286,6 @@ class X3BwdStreamPacker(X3StreamPacker):
         mats += [("pts_linears.0.weight", enc, act)]
         out, off = [], 0
         for j, (name, rmap, cmap) in enumerate(mats):
-            if not self.with_enc and j in (4, 10):
-                out.append((name, rmap, cmap, None, j))
-                continue
             out.append((name, rmap, cmap, off, j))
             off += -(-len(rmap) * len(cmap) // 8192)
         return out, off
@@ -259,47 +295,131 @@ class X3BwdStreamPacker(X3StreamPacker):
         from .pack import H_ALPHA_W, H_RGB_W, HEAD_FLOATS, SLICE_FLOATS, _group_pack
         dev = self.device
         plan, nsl = self.plan()
+        self.recs, self.heads, self._keep, self._tables = [], [], [], (None, None)
         self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
         self.sw = torch.zeros(11, device=dev, dtype=torch.int32)
-        self.maps, recs = [], []
+        self.amax = torch.zeros(11, device=dev, dtype=torch.int32)
         for name, rmap, cmap, off, j in plan:
-            if off is None:
-                continue
-            W = p[name]
-            rm = torch.tensor(rmap, dtype=torch.int32, device=dev)
-            cm = torch.tensor(cmap, dtype=torch.int32, device=dev)
-            self.maps += [rm, cm]
             # transposed: element (i, k) = W[cmap[k]][rmap[i]]
-            recs.append((W.data_ptr(), W.stride(1), W.stride(0), rm.data_ptr(), cm.data_ptr(),
-                         len(rmap), len(cmap), self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
-                         self.sw[j:j + 1].data_ptr()))
-        dt = np.dtype([("src", "<u8"), ("ldr", "<i8"), ("ldc", "<i8"), ("rowmap", "<u8"),
-                       ("colmap", "<u8"), ("M", "<i4"), ("K", "<i4"), ("out", "<u8"),
-                       ("sw", "<u8")])
-        self.table = torch.from_numpy(np.array(recs, dtype=dt).view(np.uint8).copy()).to(dev)
+            self._matrix(p[name], rmap, cmap, True, self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
+                         self.sw[j:j + 1].data_ptr(), self.amax[j:j + 1].data_ptr())
         # head: rgb W [3][4][32] and alpha W [4][64] lane-packed (pack_mlp's layout),
-        # then the scales: src = cat(rgb W (384), alpha W (256), sw (11))
+        # then the scales: sources = cat(rgb W (384), alpha W (256)), scales
         idx = np.full(HEAD_FLOATS, -1, np.int64)
         rgb_idx = np.arange(384).reshape(3, 128)
         for c in range(3):
             idx[H_RGB_W + c * 128:H_RGB_W + c * 128 + 128] = _group_pack(rgb_idx[c], 8).reshape(-1)
         idx[H_ALPHA_W:H_ALPHA_W + 256] = 384 + _group_pack(np.arange(256), 16).reshape(-1)
         idx[3100:3111] = 640 + np.arange(11)
-        keep = np.nonzero(idx >= 0)[0]
-        self.head_dst = torch.from_numpy(keep).to(dev)
-        self.head_src = torch.from_numpy(idx[keep]).to(dev)
         self.head = torch.zeros(HEAD_FLOATS, device=dev, dtype=torch.float32)
+        self._head(_src_pointers(p, ["rgb_linear.weight", "alpha_linear.weight"], idx,
+                                 self.amax, 640), self.head)
 
     def pack(self, p):
         key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
         if key != self.key:
             self._build(p)
             self.key = key
-        call("nerf_x3_pack", ptr(self.table), len(self.maps) // 2, _lib.stream_of(self.device))
-        src = torch.cat([p["rgb_linear.weight"].detach().reshape(-1),
-                         p["alpha_linear.weight"].detach().reshape(-1), self.sw.float()])
-        self.head.index_copy_(0, self.head_dst, src.index_select(0, self.head_src))
+        self.launch()
         return self.stream, self.head
+
+
+class X3NetPacker:
+    """Both fused kernels' streams of one network (X3StreamPacker for the
+    forward, X3BwdStreamPacker for the backward), packed together by one
+    nerf_x3_pack launch set at the network's forward (the backward of that
+    forward reads the same parameters: autograd forbids changing them in
+    between), so a training step packs each network once; prepack() packs
+    several networks in one launch set for their next forwards."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.fwd = X3StreamPacker(device)
+        self.bwd = X3BwdStreamPacker(device)
+        self.key = None         # storage key of the built tables
+        self.pending = False    # packed by prepack() for the next streams() call
+
+    def _ensure_built(self, p):
+        key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
+        if key != self.key:
+            self.fwd._build(p)
+            self.bwd._build(p)
+            self.fwd.key = self.bwd.key = self.key = key
+            self.pending = False
+
+    def records(self):
+        return self.fwd.recs + self.bwd.recs, self.fwd.heads + self.bwd.heads
+
+    def streams(self, p):
+        """(fwd stream, fwd head, bwd stream, bwd head) of the live parameters:
+        packed now, unless prepack() just did."""
+        self._ensure_built(p)
+        if not self.pending:
+            _launch_packs([self])
+        self.pending = False
+        return self.fwd.stream, self.fwd.head, self.bwd.stream, self.bwd.head
+
+    def invalidate(self):
+        self.pending = False
+
+
+_PACK_TABLES = {}
+
+
+def _launch_packs(nets):
+    """One nerf_x3_pack launch set over several networks' records (the tables
+    cached per set of built packers)."""
+    key = tuple((id(n), n.key) for n in nets)
+    tabs = _PACK_TABLES.get(key)
+    if tabs is None:
+        recs, heads = [], []
+        for n in nets:
+            r, h = n.records()
+            recs += r
+            heads += h
+        dev = nets[0].device
+        if len(_PACK_TABLES) > 64:
+            _PACK_TABLES.clear()
+        tabs = _PACK_TABLES[key] = (_device_table(recs, _DESC_FIELDS, dev), len(recs),
+                                    _device_table(heads, _HEAD_FIELDS, dev), len(heads))
+    descs, n, htab, nh = tabs
+    call("nerf_x3_pack", ptr(descs), n, ptr(htab), nh, _lib.stream_of(nets[0].device))
+
+
+_NETS = {}
+
+
+def _net_for(params, device):
+    p = dict(zip(PARAM_NAMES, params))
+    key = p["pts_linears.0.weight"].data_ptr()
+    net = _NETS.get(key)
+    if net is None:
+        net = _NETS[key] = X3NetPacker(device)
+    return net, p
+
+
+def prepack(networks):
+    """Pack the fused kernels' streams of several networks (each a list of its
+    24 parameters in PARAM_NAMES order, or a NeRF module) in ONE launch set;
+    each network's next forward uses them instead of packing (a training step
+    calls it right before its forwards, after the previous optimizer step)."""
+    nets = []
+    for params in networks:
+        if isinstance(params, torch.nn.Module):
+            params = mlp_params(params)
+        net, p = _net_for(params, params[0].device)
+        net._ensure_built(p)
+        nets.append(net)
+    if nets:
+        _launch_packs(nets)
+        for n in nets:
+            n.pending = True
+
+
+def invalidate_packs():
+    """Drop prepack()'s packing: every network's next forward packs again."""
+    for net in _NETS.values():
+        net.invalidate()
 
 
 class _BwdIO(ctypes.Structure):
@@ -308,38 +428,21 @@ class _BwdIO(ctypes.Structure):
                 ("d", ctypes.c_void_p * 12), ("dmax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
 
 
-_BWD_STREAMS = {}
-
-
-def _bwd_stream_for(params, device, with_enc):
-    p = dict(zip(PARAM_NAMES, params))
-    key = (p["pts_linears.0.weight"].data_ptr(), bool(with_enc))
-    pk = _BWD_STREAMS.get(key)
-    if pk is None:
-        pk = _BWD_STREAMS[key] = X3BwdStreamPacker(device, with_enc)
-    return pk.pack(p)
-
-
 class _TrainOut(ctypes.Structure):
     """NerfX3TrainOut (include/nerfhip.h)."""
-    _fields_ = [("act", ctypes.c_void_p * 10), ("bits", ctypes.c_void_p * 9),
+    _fields_ = [("act", ctypes.c_void_p * 12), ("bits", ctypes.c_void_p * 9),
                 ("amax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
 
 
 _PACKERS = {}
-_STREAMS = {}
 _ZERO = {}
 
 
-def _stream_for(params, device):
-    """(stream, head) of the network whose parameters these are (one packer per
-    network, keyed by the first weight's storage)."""
-    p = dict(zip(PARAM_NAMES, params))
-    key = p["pts_linears.0.weight"].data_ptr()
-    pk = _STREAMS.get(key)
-    if pk is None:
-        pk = _STREAMS[key] = X3StreamPacker(device)
-    return pk.pack(p)
+def _streams_for(params, device):
+    """(fwd stream, fwd head, bwd stream, bwd head) of the network whose
+    parameters these are, for its forward and that forward's backward."""
+    net, p = _net_for(params, device)
+    return net.streams(p)
 
 
 def _packs_for(params, device, forward=True, backward=True):
@@ -423,15 +526,53 @@ class _WgradDesc(ctypes.Structure):
                 ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int)]
 
 
+_NCU = {}
+
+
+def _n_cu(device):
+    d = torch.device(device)
+    if d not in _NCU:
+        _NCU[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _NCU[d]
+
+
 def _dma_ok(t):
     return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
 
 
+WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "128"))
+
+
+def wgrad_tile_chunks(shapes, P, n_cu=256, floor=None):
+    """K split of every 256 x 256 output tile of a batched weight-gradient
+    launch (order: descriptor, N tile, M tile): proportional to the operand
+    rows the tile streams per K step (A rows + B rows, at least 128: a step
+    has fixed costs), scaled so all tiles' workgroups fit one per CU -- a
+    light tile (the heads, the 32- / 64-row remainders) finishes its share
+    of the samples as late as a full one. shapes: (M, N) per descriptor."""
+    costs = []
+    for M, N in shapes:
+        for j in range(-(-N // 256)):
+            for i in range(-(-M // 256)):
+                rows = min(256, M - 256 * i) + min(256, N - 256 * j)
+                costs.append(max(rows, WGRAD_COST_FLOOR if floor is None else floor) / 512.0)
+    cap = max(1, min(P // 32, 255))
+    zs = [1] * len(costs)
+    lam = 1.0
+    while True:   # the largest scale whose workgroups fit the CUs
+        nz = [max(1, min(cap, int(c * lam))) for c in costs]
+        if sum(nz) > n_cu or nz == zs and lam > 4 * n_cu:
+            break
+        zs = nz
+        lam *= 1.02
+    return zs
+
+
 class WgradBatch:
     """The weight gradients of one backward, deferred and computed together by
-    ONE nerf_x3_wgrad_batch launch (each split over ~256 / tiles sample subsets,
-    so the split-K partials are ~10x fewer than per-layer launches), then ONE
-    fixed-order partial sum for all weights and one for all biases.
+    ONE nerf_x3_wgrad_batch_z launch (each 256 x 256 output tile split over
+    sample subsets, the split sized to the tile's rows: wgrad_tile_chunks), then
+    ONE fixed-order partial sum for all weights and one for all biases.
     add() returns a slot; results()[slot] = (dW[, db]). Requests whose operands
     the batched kernel cannot take (P % 32, alignment) run through _wgrad."""
 
@@ -458,8 +599,8 @@ class WgradBatch:
                   for A, B, *_ in req))
         if not ok:
             return [_wgrad(A, B, aa, ab, wb) for A, B, aa, ab, wb in req]
-        tiles = sum(-(-A.shape[0] // 256) * -(-B.shape[0] // 256) for A, B, *_ in req)
-        Z = max(1, min(P // 32, 256 // tiles))
+        zs = wgrad_tile_chunks([(A.shape[0], B.shape[0]) for A, B, *_ in req], P, _n_cu(self.device))
+        Z = max(zs)
         sizes = [A.shape[0] * B.shape[0] for A, B, *_ in req]
         bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb in req]
         ld, ldb = sum(sizes), max(1, sum(bsizes))
@@ -475,7 +616,8 @@ class WgradBatch:
             off += sizes[k]
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
-        call("nerf_x3_wgrad_batch", ctypes.addressof(descs), len(req), Z, st)
+        zarr = (ctypes.c_int * len(zs))(*zs)
+        call("nerf_x3_wgrad_batch_z", ctypes.addressof(descs), len(req), zarr, Z, st)
         flat = torch.empty((ld,), device=self.device, dtype=torch.float32)
         call("nerf_sum_partials", ptr(part), Z, ld, ptr(flat), st)
         bflat = torch.empty((ldb,), device=self.device, dtype=torch.float32)
@@ -515,7 +657,6 @@ HEAD_SRC = ([f"pts_linears.{i}.bias" for i in range(8)] +
 # (nerf_mlp_train_backward_x3); NERF_TRAIN_FUSED_FORWARD=0 /
 # NERF_TRAIN_FUSED_BACKWARD=0 select the layer launches (the parity tests run
 # both).
-import os as _os
 FUSED_FORWARD = _os.environ.get("NERF_TRAIN_FUSED_FORWARD", "1") != "0"
 FUSED_BACKWARD = _os.environ.get("NERF_TRAIN_FUSED_BACKWARD", "1") != "0"
 
@@ -556,15 +697,18 @@ class NerfMLPFn(torch.autograd.Function):
         # 10 = view encoding (both from the encoding kernel), 11 = views layer
         amax = torch.zeros(12, device=dev, dtype=f32)
         pts_c = pts.detach().contiguous()
-        _encode(pts_c, XYZ_FREQS, E, amax[9:10])                   # E[:63] = enc^T
-        E[63].zero_()                                              # h4 rows: layer 4
-        H = [_act(256, P, dev) if i not in (4,) else None
+        fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
+        if not fused_f:   # (the fused forward writes the encoding rows itself)
+            _encode(pts_c, XYZ_FREQS, E, amax[9:10])               # E[:63] = enc^T
+            E[63].zero_()
+        H = [_act(256, P, dev) if i not in (4,) else None          # h4 rows: layer 4
              for i in range(8)]
         H[4] = E[64:320]
-        fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
         pk = None if fused_f and fused_b else \
             _packs_for(params, dev, forward=not fused_f, backward=not fused_b)
         ctx.fused_backward = fused_b
+        # the fused kernels' weight streams (both directions, one packing)
+        ctx.streams = _streams_for(params, dev) if fused_f or fused_b else None
         if fused_f:
             return NerfMLPFn._forward_fused(ctx, pts, pts_c, dirs, params, E, H, amax, pk)
         src = E[0:64]
@@ -606,11 +750,9 @@ class NerfMLPFn(torch.autograd.Function):
         unfused forward produce, and the backward reads."""
         dev = pts.device
         P = pts.shape[0]
-        stream, head = _stream_for(params, dev)
-        V = _act(288, P, dev)                                      # cat(feature, views enc)
-        V[283:].zero_()
+        stream, head = ctx.streams[:2]
+        V = _act(288, P, dev)      # cat(feature, views enc, 5 zero rows): all from the kernel
         dirs_c = dirs.detach().contiguous()
-        _encode(dirs_c, DIR_FREQS, V[256:283], amax[10:11])
         HV = _act(128, P, dev)
         bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
         bits_v = torch.empty((relu_bits_words(P, 8),), device=dev, dtype=torch.int16)
@@ -624,6 +766,8 @@ class NerfMLPFn(torch.autograd.Function):
             out.bits[i] = bits[i].data_ptr()
         out.act[8] = V[0:256].data_ptr()
         out.act[9] = HV.data_ptr()
+        out.act[10] = E[0:64].data_ptr()
+        out.act[11] = V[256:288].data_ptr()
         out.bits[8] = bits_v.data_ptr()
         out.amax = amax.data_ptr()
         out.ld = H[0].stride(0)
@@ -645,20 +789,29 @@ class NerfMLPFn(torch.autograd.Function):
         P = d_raw.shape[0]
         f32 = torch.float32
         grads = {}
-        DR = torch.zeros((32, P), device=dev, dtype=f32)   # d_raw^T: the K step of d hv
+        # d_raw^T (the rgb / alpha heads' wgrad operands; the layer launches'
+        # d hv K step: 32 rows, 4 of them d_raw)
+        DR = torch.empty((4, P), device=dev, dtype=f32) if ctx.fused_backward else \
+            torch.zeros((32, P), device=dev, dtype=f32)
         DR[:4].copy_(d_raw.t())
         d_rgb, d_sig = DR[0:3], DR[3:4]
         wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
         post = {}              # slot -> (weight name, bias name or None, column fix-up)
+        # max |d| of each product (slots as NerfX3BwdIO.dmax); [11] / [12]: of
+        # d rgb / d sigma (one pass over d_raw)
+        dmax = torch.zeros(13, device=dev, dtype=f32)
+        d_raw_c = d_raw.detach().to(f32).contiguous()
+        if d_raw_c.data_ptr() % 16:
+            d_raw_c = d_raw_c.clone()
+        call("nerf_raw_absmax", ptr(d_raw_c), P, ptr(dmax[11:]), _lib.stream_of(dev))
         # the heads' bias gradients come out of the batched launch too (its row
         # sums), not from separate reductions over P
-        post[wb.add(d_rgb, HV, amax_b=amax[11:12], with_bias=True)] = (
+        post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
-        dmax = torch.zeros(11, device=dev, dtype=f32)   # max |d| of each layer-kernel output
         need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
         if ctx.fused_backward:
-            d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(d_raw, params, bits, bits_v, dmax,
-                                                           need_enc)
+            d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(d_raw_c, ctx.streams[2:], bits, bits_v,
+                                                           dmax, need_enc)
         else:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
                                                             need_enc)
@@ -667,7 +820,7 @@ class NerfMLPFn(torch.autograd.Function):
             "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
         post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
             "feature_linear.weight", "feature_linear.bias", None)
-        post[wb.add(d_sig, H[7], amax_b=amax[7:8], with_bias=True)] = (
+        post[wb.add(d_sig, H[7], dmax[12:13], amax[7:8], with_bias=True)] = (
             "alpha_linear.weight", "alpha_linear.bias", None)
         for i in range(7, -1, -1):
             inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
@@ -684,16 +837,18 @@ class NerfMLPFn(torch.autograd.Function):
             if bname:
                 grads[bname] = gb
         d_pts = None
-        if d_enc is not None:
+        if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
             d_pts = torch.empty((P, 3), device=dev, dtype=f32)
-            call("nerf_freq_encode_fm_backward", ptr(d_enc), d_enc.stride(0), ptr(pts), 3, P,
-                 XYZ_FREQS, ptr(d_pts), _lib.stream_of(dev))
+            assert d_enc[0].stride(0) == d_enc[1].stride(0)
+            call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]),
+                 d_enc[0].stride(0), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts), _lib.stream_of(dev))
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
 
 
 def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
     """The backward's chain of products as layer launches: d hv, DF, D0..D7 and
-    (need_enc) the encoding gradient rows, dmax raised as the fused kernel does."""
+    (need_enc) the encoding gradient rows of layers 5 and 0, dmax raised as the
+    fused kernel does."""
     dev = DR.device
     P = DR.shape[1]
     d_hv = _act(128, P, dev)   # d hv = (W_rgb^T d_rgb) * (hv > 0): the views layer's ReLU bits
@@ -718,29 +873,28 @@ def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
             _layer(wt, swt, mt, nk, D[5], D[4], P, mask_bits=bits[4], amax=dmax[4:5])
             if need_enc:
                 we, swe, mt, nk = pk["bwd5e"]
-                de = _act(64, P, dev)
-                _layer(we, swe, mt, nk, D[5], de, P)
-                d_enc = de[:63]
+                de5 = _act(64, P, dev)
+                _layer(we, swe, mt, nk, D[5], de5, P)
         else:
             wt, swt, mt, nk = pk[f"bwd{i}"]
             _layer(wt, swt, mt, nk, D[i], D[i - 1], P, mask_bits=bits[i - 1],
                    amax=dmax[i - 1:i])
     if need_enc:
         wt, swt, mt, nk = pk["bwd0"]
-        de = _act(64, P, dev)
-        _layer(wt, swt, mt, nk, D[0], de, P)
-        d_enc = de[:63] if d_enc is None else d_enc + de[:63]
+        de0 = _act(64, P, dev)
+        _layer(wt, swt, mt, nk, D[0], de0, P)
+        d_enc = (de5[:63], de0[:63])
     return d_hv, DF, D, d_enc
 
 
-def _backward_fused_impl(d_raw, params, bits, bits_v, dmax, need_enc):
+def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc):
     """The same chain as ONE nerf_mlp_train_backward_x3 launch over the
     transposed weight stream (X3BwdStreamPacker): every product's rows written
     feature-major and its max |.| raised, the ReLU masks from the forward's
-    bits; d_enc = the layer-5 and layer-0 encoding rows summed."""
+    bits; d_enc = the layer-5 and layer-0 encoding rows."""
     dev = d_raw.device
     P = d_raw.shape[0]
-    stream, head = _bwd_stream_for(params, dev, need_enc)
+    stream, head = streams
     d_raw_c = d_raw.detach().to(torch.float32).contiguous()
     if d_raw_c.data_ptr() % 16:
         d_raw_c = d_raw_c.clone()
@@ -762,7 +916,7 @@ def _backward_fused_impl(d_raw, params, bits, bits_v, dmax, need_enc):
     assert all(t.stride(0) == io.ld for t in [DF, d_hv] + ([de5, de0] if need_enc else []))
     call("nerf_mlp_train_backward_x3", ptr(stream), ptr(head), P, int(bool(need_enc)),
          ctypes.addressof(io), _lib.stream_of(dev))
-    d_enc = de5[:63] + de0[:63] if need_enc else None
+    d_enc = (de5[:63], de0[:63]) if need_enc else None
     return d_hv, DF, D, d_enc
 
 

@@ -335,11 +335,10 @@ def test_x3_stream_packer_matches_host_packing(dev):
     assert torch.equal(head.cpu(), torch.from_numpy(ref_h))
 
 
-@pytest.mark.parametrize("with_enc", [True, False])
-def test_x3_bwd_stream_packer_matches_host_packing(dev, with_enc):
+def test_x3_bwd_stream_packer_matches_host_packing(dev):
     """X3BwdStreamPacker: every transposed matrix's slices == pack_x3_matrix of
     that matrix (rows / K columns through the plan's maps, -1 -> 0) bit for bit,
-    at the slice offsets the backward kernel consumes (72 / 68 slices); the
+    at the slice offsets the backward kernel consumes (72 slices); the
     head's rgb / alpha weights where the forward head holds them, the scales at
     3100 + matrix index."""
     import numpy as np
@@ -347,14 +346,12 @@ def test_x3_bwd_stream_packer_matches_host_packing(dev, with_enc):
     from nerfhip.train_mlp import PARAM_NAMES, X3BwdStreamPacker, mlp_params, pack_x3_matrix
     m = _model(dev, seed=3, gain=2.5)
     p = dict(zip(PARAM_NAMES, mlp_params(m)))
-    pk = X3BwdStreamPacker(dev, with_enc)
+    pk = X3BwdStreamPacker(dev)
     stream, head = pk.pack(p)
     plan, nsl = pk.plan()
-    assert nsl == (72 if with_enc else 68) and stream.numel() == nsl * SLICE_FLOATS
+    assert nsl == 72 and stream.numel() == nsl * SLICE_FLOATS
     hd = head.cpu()
     for name, rmap, cmap, off, j in plan:
-        if off is None:
-            continue
         Wt = p[name].detach().t()
         rm, cm = torch.tensor(rmap, device=dev), torch.tensor(cmap, device=dev)
         T = torch.where((rm >= 0)[:, None] & (cm >= 0)[None, :],
@@ -431,7 +428,7 @@ def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatc
     def recording(key, fn, dmax_arg):
         def w(*a):
             out = fn(*a)
-            rows = [out[0], out[1], *out[2]] + ([out[3]] if out[3] is not None else [])
+            rows = [out[0], out[1], *out[2]] + (list(out[3]) if out[3] is not None else [])
             rec[key] = ([t.clone() for t in rows], a[dmax_arg].clone(), out[3] is None)
             return out
         return staticmethod(w)
@@ -448,14 +445,50 @@ def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatc
         wrt = ([y] if pts_grad else []) + mlp_params(m)
         grads[fused] = torch.autograd.grad(out, wrt, d_raw)
     (r0, m0, n0), (r1, m1, n1) = rec[False], rec[True]
-    assert n0 == n1 == (not pts_grad) and len(r0) == len(r1) == (11 if pts_grad else 10)
-    names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc"]
+    assert n0 == n1 == (not pts_grad) and len(r0) == len(r1) == (12 if pts_grad else 10)
+    names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc5", "d_enc0"]
     for name, a, b in zip(names, r1, r0):
         assert a.shape == b.shape, name
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
-        if name not in ("DF", "d_enc"):   # masked products: the same zeros
+        if name not in ("DF", "d_enc5", "d_enc0"):   # masked products: the same zeros
             assert float(((a == 0) != (b == 0)).float().mean()) <= 1e-6, name
-    slots = [0, 1, 2, 3, 4, 5, 6, 7, 8, 10]
-    assert torch.allclose(m1[slots], m0[slots], rtol=1e-5, atol=0), (m1, m0)
+    assert torch.allclose(m1, m0, rtol=1e-5, atol=0), (m1, m0)
     for name, a, b in zip((["pts"] if pts_grad else []) + PARAM_NAMES, grads[True], grads[False]):
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
+
+
+def test_net_packer_packs_live_parameters(dev):
+    """X3NetPacker: a network's two fused streams at each forward are a packing
+    of the live parameters (after a fused-Adam step they equal a fresh packing
+    of the updated ones); prepack of two networks in one launch set == each
+    packed alone, and is used by their next forwards."""
+    from nerfhip import train_mlp
+    from nerfhip.train_mlp import (PARAM_NAMES, X3BwdStreamPacker, X3StreamPacker, mlp_params,
+                                   prepack)
+    m = _model(dev, seed=3, gain=2.5)
+    m2 = _model(dev, seed=5, gain=2.0)
+    fs0 = train_mlp._streams_for(mlp_params(m), dev)[0].clone()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, fused=True)
+    sum((p * p).sum() for p in m.parameters()).backward()
+    opt.step()
+
+    def check(mod, got):
+        p = dict(zip(PARAM_NAMES, mlp_params(mod)))
+        rs, rh = X3StreamPacker(dev).pack(p)
+        rbs, rbh = X3BwdStreamPacker(dev).pack(p)
+        fs, fh, bs, bh = got
+        assert torch.equal(fs.view(torch.int32), rs.view(torch.int32)) and torch.equal(fh, rh)
+        assert torch.equal(bs.view(torch.int32), rbs.view(torch.int32)) and torch.equal(bh, rbh)
+
+    check(m, train_mlp._streams_for(mlp_params(m), dev))
+    assert not torch.equal(train_mlp._streams_for(mlp_params(m), dev)[0].view(torch.int32),
+                           fs0.view(torch.int32))
+    with torch.no_grad():
+        for q in list(m.parameters()) + list(m2.parameters()):
+            q.mul_(0.5)
+    prepack([m, m2])
+    nets = [train_mlp._net_for(mlp_params(x), dev)[0] for x in (m, m2)]
+    assert all(n.pending for n in nets)
+    check(m, train_mlp._streams_for(mlp_params(m), dev))     # prepack's packing, not a new one
+    check(m2, train_mlp._streams_for(mlp_params(m2), dev))
+    assert not any(n.pending for n in nets)

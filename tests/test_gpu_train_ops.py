@@ -121,3 +121,51 @@ def test_sample_fine_forward_bit_exact_and_backward(dev, S, NI):
     err = (got.double() - exp.double()).abs().amax(1) / exp.abs().amax().double().clamp_min(1e-30)
     assert float((err < 1e-4).double().mean()) >= 0.99, float(err.max())
     assert float(err.max()) < 1e-2
+
+
+@pytest.mark.parametrize("P", [1, 1000, 196608, 300001])
+def test_raw_absmax_matches_torch(dev, P):
+    """nerf_raw_absmax (the rgb / alpha heads' weight-gradient scales): max |rgb|
+    and max |sigma| of d_raw, exactly torch's amax (order-free), raising the
+    caller's slots (never lowering them)."""
+    from nerfhip._lib import call, ptr, stream_of
+    g = torch.Generator(device=dev).manual_seed(P)
+    raw = torch.randn((P, 4), device=dev, generator=g) * torch.tensor([1.0, 2.0, 3.0, 0.5],
+                                                                      device=dev)
+    out = torch.zeros(2, device=dev)
+    call("nerf_raw_absmax", ptr(raw), P, ptr(out), stream_of(dev))
+    assert out[0].item() == raw[:, :3].abs().max().item()
+    assert out[1].item() == raw[:, 3].abs().max().item()
+    big = torch.full((2,), 1e6, device=dev)
+    call("nerf_raw_absmax", ptr(raw), P, ptr(big), stream_of(dev))
+    assert torch.equal(big, torch.full((2,), 1e6, device=dev))
+
+
+def test_x3_clock_twin_computes_the_same(dev):
+    """nerf_mlp_forward_x3_clock (bench.py's held-clock probe) gives
+    nerf_mlp_forward_x3's raw bit for bit, and one stamp per workgroup whose
+    clock (d memtime / d realtime x 100 MHz) is a plausible shader clock."""
+    from nerfhip._lib import call, ptr, stream_of
+    from nerfhip.pack import pack_mlp_x3
+    from nerfhip.synthetic import make_params
+    sl, hd = (torch.from_numpy(a).to(dev) for a in pack_mlp_x3(make_params(0, 2.0, 0.1)))
+    n, S = 5000, 64
+    g = torch.Generator(device=dev).manual_seed(3)
+    ro = torch.rand((n, 3), device=dev, generator=g) - 0.5
+    rd = torch.nn.functional.normalize(torch.randn((n, 3), device=dev, generator=g), dim=1)
+    z = torch.linspace(2.0, 6.0, S, device=dev)
+    a = torch.empty((n * S, 4), device=dev)
+    b = torch.empty((n * S, 4), device=dev)
+    call("nerf_mlp_forward_x3", ptr(sl), ptr(hd), ptr(ro), ptr(rd), ptr(z), 0, n, S, ptr(a),
+         stream_of(dev))
+    clk = torch.zeros(4 * 4096, device=dev, dtype=torch.int64)
+    trace = torch.zeros(512 * 4, device=dev, dtype=torch.int64)
+    call("nerf_mlp_forward_x3_clock", ptr(sl), ptr(hd), ptr(ro), ptr(rd), ptr(z), 0, n, S, ptr(b),
+         ptr(clk), clk.numel(), ptr(trace), stream_of(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    c = clk.view(-1, 4).cpu().numpy().astype(np.float64)
+    used = c[:, 3] > c[:, 2]
+    assert used.sum() == min(-(-n * S // 128), torch.cuda.get_device_properties(dev).multi_processor_count)
+    ghz = (c[used, 1] - c[used, 0]) / (c[used, 3] - c[used, 2]) * 0.1
+    assert 0.5 < np.median(ghz) < 3.0, np.median(ghz)

@@ -34,7 +34,7 @@ def main(P=1000):
         def w(*a, fn=fn, key=key, di=di):
             out = fn(*a)
             torch.cuda.synchronize()
-            rows = [out[0], out[1], *out[2]] + ([out[3]] if out[3] is not None else [])
+            rows = [out[0], out[1], *out[2]] + (list(out[3]) if out[3] is not None else [])
             rec[key] = ([t.clone() for t in rows], a[di].clone())
             return out
         setattr(NerfMLPFn, attr, staticmethod(w))
@@ -45,7 +45,7 @@ def main(P=1000):
         out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
         grads[fused] = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
         torch.cuda.synchronize()
-    names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc"]
+    names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc5", "d_enc0"]
     for name, a, b in zip(names, rec[True][0], rec[False][0]):
         e = (a - b).abs()
         rel = float(e.max() / b.abs().max().clamp_min(1e-30))

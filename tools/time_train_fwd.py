@@ -44,6 +44,10 @@ def main(P=196608, reps=20):
         out.bits[i] = bits[i].data_ptr()
     out.act[8] = H[8].data_ptr()
     out.act[9] = HV.data_ptr()
+    E = _act(64, P, dev)
+    DV = _act(32, P, dev)
+    out.act[10] = E.data_ptr()
+    out.act[11] = DV.data_ptr()
     out.bits[8] = bits_v.data_ptr()
     out.amax = amax.data_ptr()
     out.ld = H[0].stride(0)
