@@ -109,6 +109,23 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
  * d_weights [n][S] (rows 0 and S-1 zero) from g_zall [n][S + n_imp]. z [n][S],
  * weights [n][S], u [n][n_imp] as given to the forward. S <= 130,
  * n_imp <= 256. */
+/* nerf_adam_step: one Adam step (torch.optim.Adam with weight_decay 0, no
+ *   amsgrad; trainers/trainer.py's optimizer) over n <= 64 parameter tensors in
+ *   ONE launch, each gradient first clamped in place to [-clip, clip]
+ *   (clip_grad_value_, trainer.py:59; clip <= 0: no clamp). tensors: host
+ *   array {p, g, m (exp_avg), v (exp_avg_sq), n} (device float pointers).
+ *   lr, step: device floats (the step count before this step; the launch
+ *   leaves step + 1); done: a device u32, 0 between launches. */
+typedef struct NerfAdamTensor {
+  float* p;
+  float* g;
+  float* m;
+  float* v;
+  int64_t n;
+} NerfAdamTensor;
+int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float* step,
+                   unsigned* done, double beta1, double beta2, float eps, float clip,
+                   nerf_stream_t stream);
 /* nerf_sum_partials: out[i] = sum_{c=0}^{C-1} part[c * n + i], summed in c
  *   order (the weight-gradient split-K partials of nerf_x3_wgrad). */
 int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream);
@@ -278,11 +295,13 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
  *   feature-major [3 + 6 * n_freq][ldd]. */
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream);
-/* The same on d_enc + d_enc2 (elementwise, same row stride): the encoding's
- * two consumers' gradients summed in the kernel. */
+/* The same on d_enc + d_enc2 (elementwise, same row stride; d_enc2
+ * nullable): the encoding's two consumers' gradients summed in the kernel.
+ * enc (nullable): the forward's encoding rows (nerf_freq_encode_fm's layout,
+ * stride ldd), whose sin / cos values are read instead of recomputed. */
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                     const float* x, int64_t ldx, int64_t P, int n_freq,
-                                     float* dx, nerf_stream_t stream);
+                                     const float* enc, const float* x, int64_t ldx, int64_t P,
+                                     int n_freq, float* dx, nerf_stream_t stream);
 /* nerf_x3_pack: packs n weight matrices for the x3 training kernels in one
  * launch set. descs (device) = n records {const float* src; int64_t ldr, ldc;
  * const int* rowmap; const int* colmap; int M, K; void* out; int* sw;

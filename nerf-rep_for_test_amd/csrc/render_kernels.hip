@@ -771,10 +771,13 @@ __global__ __launch_bounds__(64 * kEncMaxWaves) void freq_encode_fm_kernel(
 // d x_c = d_enc[c] + sum_f 2^f (cos(2^f x_c) d_sin - sin(2^f x_c) d_cos): the
 // chain rule through the encoding (autograd of freq.py's cat of sin/cos).
 // With d_enc2, d_enc = d_enc + d_enc2 elementwise first (the encoding feeds two
-// layers: autograd's sum of their input gradients).
+// layers: autograd's sum of their input gradients). With enc (the forward's
+// encoding rows, stride ldd), sin / cos are read from it instead of recomputed
+// (the same sincosf values: it is what the forward wrote).
 __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
     const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
-    const float* __restrict__ x, int64_t ldx, int64_t P, int L, float* __restrict__ dx) {
+    const float* __restrict__ enc, const float* __restrict__ x, int64_t ldx, int64_t P, int L,
+    float* __restrict__ dx) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   auto de = [&](int row) {
@@ -788,9 +791,13 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
     float g = de(c);
     for (int f = 0; f < L; ++f) {
       const float k = (float)(1 << f);
-      const float a = v * k;
       float sn, cs;
-      sincosf(a, &sn, &cs);
+      if (enc) {
+        sn = enc[(3 + 6 * f + c) * ldd + p];
+        cs = enc[(6 + 6 * f + c) * ldd + p];
+      } else {
+        sincosf(v * k, &sn, &cs);
+      }
       const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
       g = g + ds * k;
     }
@@ -986,18 +993,19 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
 
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream) {
-  return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, x, ldx, P, n_freq, dx, stream);
+  return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, nullptr, x, ldx, P, n_freq, dx,
+                                          stream);
 }
 
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                     const float* x, int64_t ldx, int64_t P, int n_freq,
-                                     float* dx, nerf_stream_t stream) {
+                                     const float* enc, const float* x, int64_t ldx, int64_t P,
+                                     int n_freq, float* dx, nerf_stream_t stream) {
   NERF_REQUIRE(d_enc && x && dx, "nerf_freq_encode_fm_backward: null pointer");
   NERF_REQUIRE(P >= 0 && ldx >= 3 && ldd >= P && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm_backward: bad size");
   if (P == 0) return 0;
   hipLaunchKernelGGL(freq_encode_fm_backward_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
-                     as_stream(stream), d_enc, d_enc2, ldd, x, ldx, P, n_freq, dx);
+                     as_stream(stream), d_enc, d_enc2, ldd, enc, x, ldx, P, n_freq, dx);
   return check_launch("freq_encode_fm_backward_kernel");
 }
 

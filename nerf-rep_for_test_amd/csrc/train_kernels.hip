@@ -440,6 +440,98 @@ int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_
   return check_launch("sum_partials_kernel");
 }
 
+int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float* step,
+                   unsigned* done, double beta1, double beta2, float eps, float clip,
+                   nerf_stream_t stream);
+
 }  // extern "C"
+
+// One Adam step (trainers' torch.optim.Adam, weight decay 0, no amsgrad) over
+// every parameter of the step in ONE launch, the gradient first clamped to
+// [-clip, clip] in place (clip_grad_value_, trainer.py:59; clip <= 0: none),
+// in torch's single-tensor Adam's float32 operation order (lerp, mul +
+// addcmul, addcdiv; the bias corrections in double, as its Python scalars):
+//   m = m + (1 - b1) (g - m),  v = v b2 + (1 - b2) g g,
+//   p = p - lr / (1 - b1^t) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)),  t = step + 1.
+// lr and the step count live on the device (a HIP graph replays the launch);
+// the last workgroup to finish writes step = t (every workgroup read the old
+// count first).
+constexpr int kAdamMax = 64;
+constexpr int kAdamBlock = 4096;   // elements per workgroup (a few hundred workgroups:
+                                   // as many atomics on the finish counter)
+struct AdamBatch {
+  NerfAdamTensor t[kAdamMax];
+  int blk_end[kAdamMax];           // prefix sums of the tensors' workgroups
+  int nt;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const float* __restrict__ lr,
+                                                   float* __restrict__ step,
+                                                   unsigned* __restrict__ done, double beta1,
+                                                   double beta2, float eps, float clip) {
+  const int blk = (int)blockIdx.x;
+  int k = 0;
+  while (k + 1 < b.nt && blk >= b.blk_end[k]) ++k;
+  const NerfAdamTensor& T = b.t[k];
+  const int64_t base = (int64_t)(blk - (k ? b.blk_end[k - 1] : 0)) * kAdamBlock;
+  __shared__ float coef[3];
+  if (threadIdx.x == 0) {   // the bias corrections once per workgroup (double, as torch's scalars)
+    const float t = *step + 1.0f;
+    coef[0] = (float)((double)*lr / (1.0 - pow(beta1, (double)t)));
+    coef[1] = (float)sqrt(1.0 - pow(beta2, (double)t));
+    coef[2] = t;
+  }
+  __syncthreads();
+  const float step_size = coef[0], bc2s = coef[1], t = coef[2];
+  const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2), b2 = (float)beta2;
+#pragma unroll
+  for (int r = 0; r < kAdamBlock / 256; ++r) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    if (i < T.n) {
+      float g = T.g[i];
+      if (clip > 0.0f) {
+        g = fminf(fmaxf(g, -clip), clip);
+        T.g[i] = g;
+      }
+      const float m0 = T.m[i];
+      const float m = m0 + w1 * (g - m0);               // lerp (weight < 0.5)
+      const float v = T.v[i] * b2 + (w2 * g) * g;        // mul_, addcmul_
+      T.m[i] = m;
+      T.v[i] = v;
+      const float denom = sqrtf(v) / bc2s + eps;
+      T.p[i] = T.p[i] + (-step_size) * (m / denom);     // addcdiv_
+    }
+  }
+  __syncthreads();   // this workgroup's reads of *step are done
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+      *step = t;
+      *done = 0u;
+    }
+  }
+}
+
+extern "C" int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float* step,
+                              unsigned* done, double beta1, double beta2, float eps, float clip,
+                              nerf_stream_t stream) {
+  NERF_REQUIRE(tensors && lr && step && done && n >= 1 && n <= kAdamMax,
+               "nerf_adam_step: bad arguments");
+  AdamBatch b;
+  int blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    const NerfAdamTensor& T = tensors[k];
+    NERF_REQUIRE(T.p && T.g && T.m && T.v && T.n >= 0 && T.n < (1ll << 31),
+                 "nerf_adam_step: bad tensor");
+    b.t[k] = T;
+    blocks += (int)cdiv(T.n, kAdamBlock);
+    b.blk_end[k] = blocks;
+  }
+  b.nt = n;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), b, lr,
+                     step, done, beta1, beta2, eps, clip);
+  return check_launch("adam_kernel");
+}
 
 }  // namespace nerfhip

@@ -35,6 +35,7 @@ SIGNATURES = {
                            _P, _S]),
     "nerf_x3_layer_ex": (_I, [_P, _P, _I, _I, _P, _P, _I64, _P, _I64, _P, _P, _I, _P, _I64,
                               _I64, _P, _P, _P, _P, _P, _I, _P, _I, _S]),
+    "nerf_adam_step": (_I, [_P, _I, _P, _P, _P, C.c_double, C.c_double, _F, _F, _S]),
     "nerf_sum_partials": (_I, [_P, _I64, _I64, _P, _S]),
     "nerf_x3_wgrad_batch": (_I, [_P, _I, _I, _S]),
     "nerf_x3_wgrad_batch_z": (_I, [_P, _I, _P, _I, _S]),
@@ -47,7 +48,7 @@ SIGNATURES = {
     "nerf_freq_encode_fm": (_I, [_P, _I64, _I64, _I, _P, _I64, _P, _S]),
     "nerf_freq_encode_fm_backward": (_I, [_P, _I64, _P, _I64, _I64, _I, _P, _S]),
     "nerf_raw_absmax": (_I, [_P, _I64, _P, _S]),
-    "nerf_freq_encode_fm_backward_sum": (_I, [_P, _P, _I64, _P, _I64, _I64, _I, _P, _S]),
+    "nerf_freq_encode_fm_backward_sum": (_I, [_P, _P, _I64, _P, _P, _I64, _I64, _I, _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_sample_fine": (_I, [_P, _I64, _P, _P, _I64, _I64, _I, _I, _P, _S]),

@@ -264,12 +264,18 @@ class NerfTrainer:
             raise ValueError("graph=True needs ops='hip' (torch's cumprod backward syncs)")
         self.ops = ops
         self.graph = bool(graph)
-        # adam: "fused" (one fused multi-tensor kernel, the eager default) or
-        # "capturable" (step count and lr on the device; what the graph needs)
-        adam = adam or ("capturable" if self.graph else "fused")
-        if adam not in ("fused", "capturable") or (self.graph and adam != "capturable"):
-            raise ValueError("adam must be 'fused' or 'capturable' (graph: 'capturable')")
-        if adam == "capturable":
+        # adam: "hip" (the default: clip_grad_value_ + Adam in one nerf_adam_step
+        # launch, lr and step count on the device, graph-capturable), or torch's
+        # "fused" (eager only) / "capturable" multi-tensor Adam after a separate
+        # clip_grad_value_
+        adam = adam or "hip"
+        if adam not in ("hip", "fused", "capturable") or (self.graph and adam == "fused"):
+            raise ValueError("adam must be 'hip', 'fused' or 'capturable' (graph: not 'fused')")
+        self.adam = adam
+        if adam == "hip":
+            from .adam import HipAdam
+            self.opt = HipAdam(self.parameters(), lr=lr, eps=1e-8, clip=self.clip_value)
+        elif adam == "capturable":
             self.opt = torch.optim.Adam(self.parameters(),
                                         lr=torch.tensor(lr, device=self.device), eps=1e-8,
                                         weight_decay=0.0, capturable=True, foreach=True)
@@ -376,7 +382,8 @@ class NerfTrainer:
         losses["loss"].backward()
         if group is not None:   # parameters without a gradient (e.g. no fine pass) skipped
             allreduce_mean([p.grad for p in self.parameters() if p.grad is not None], group)
-        torch.nn.utils.clip_grad_value_(self.parameters(), self.clip_value)
+        if self.adam != "hip":   # (HipAdam clamps the gradients itself, in place)
+            torch.nn.utils.clip_grad_value_(self.parameters(), self.clip_value)
         self.opt.step()
         return losses
 

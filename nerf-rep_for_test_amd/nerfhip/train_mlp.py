@@ -540,7 +540,7 @@ def _dma_ok(t):
     return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
 
 
-WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "128"))
+WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "512"))
 
 
 def wgrad_tile_chunks(shapes, P, n_cu=256, floor=None):
@@ -840,8 +840,10 @@ class NerfMLPFn(torch.autograd.Function):
         if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
             d_pts = torch.empty((P, 3), device=dev, dtype=f32)
             assert d_enc[0].stride(0) == d_enc[1].stride(0)
+            assert E.stride(0) == d_enc[0].stride(0)
             call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]),
-                 d_enc[0].stride(0), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts), _lib.stream_of(dev))
+                 d_enc[0].stride(0), ptr(E), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
+                 _lib.stream_of(dev))
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
 
 

@@ -290,8 +290,8 @@ def test_graph_step_trains_and_honours_lr(dev, mlp):
 
 @pytest.mark.parametrize("explicit_draws", [True, False])
 def test_graph_step_equals_eager_steps(dev, explicit_draws):
-    """The HIP-graph step (draws and batch copied into static inputs, capturable
-    Adam with a device lr) against the eager step with the same Adam, from the
+    """The HIP-graph step (draws and batch copied into static inputs, Adam with a
+    device lr: HipAdam or torch's capturable) against the eager step with the same Adam, from the
     same weights, batches and draws: 6 steps (2 eager warm-ups, the capture, 3
     replays) give bitwise the same losses and final parameters -- a stale
     static input, a host-side branch frozen at capture or an update lost at
@@ -299,7 +299,8 @@ def test_graph_step_equals_eager_steps(dev, explicit_draws):
     device stream in the same order (t_rand, then u) from the same seed. The
     default eager trainer (fused Adam) agrees to 1e-5 over the first two steps,
     after which the reference's un-detached fine sampling makes the trajectory
-    chaotic (an ulp in a weight flips fine samples)."""
+    chaotic (an ulp in a weight flips fine samples); so does HipAdam (the default)
+    against torch's fused Adam."""
     from nerfhip.train import NerfTrainer
     z, _, ro, rd, _, _, gt = _setup(dev, "x3")
     g = torch.Generator(device=dev).manual_seed(7)
@@ -311,17 +312,61 @@ def test_graph_step_equals_eager_steps(dev, explicit_draws):
         u_ = torch.rand((n, 128), device=dev, generator=g) if explicit_draws else None
         batches.append((ro[perm], rd[perm], gt[perm], tr_, u_))
     runs = {}
-    for mode in ("eager", "eager_fused", "graph"):
+    for mode, adam in (("eager", "hip"), ("graph", "hip"), ("eager", "capturable"),
+                       ("graph", "capturable"), ("eager", "fused")):
         torch.manual_seed(99)
-        tr = NerfTrainer(dev, params_of(z), mlp="x3", graph=mode == "graph",
-                         adam="fused" if mode == "eager_fused" else "capturable")
+        tr = NerfTrainer(dev, params_of(z), mlp="x3", graph=mode == "graph", adam=adam)
         losses = [float(tr.step(*b)["loss"].item()) for b in batches]
-        runs[mode] = (np.array(losses), {k: v.clone() for k, v in tr.state().items()})
+        runs[mode, adam] = (np.array(losses), {k: v.clone() for k, v in tr.state().items()})
         if mode == "graph":
             assert len(tr._graphs) == 1
-    le, lg = runs["eager"][0], runs["graph"][0]
-    assert np.array_equal(le, lg), (le, lg)
-    for k, a in runs["eager"][1].items():
-        assert torch.equal(a, runs["graph"][1][k]), k
-    lf = runs["eager_fused"][0]
-    assert np.all(np.abs(lf[:2] - lg[:2]) <= 1e-5 * np.abs(lf[:2])), (lf, lg)
+    for adam in ("hip", "capturable"):
+        le, lg = runs["eager", adam][0], runs["graph", adam][0]
+        assert np.array_equal(le, lg), (adam, le, lg)
+        for k, a in runs["eager", adam][1].items():
+            assert torch.equal(a, runs["graph", adam][1][k]), (adam, k)
+    lf, lh = runs["eager", "fused"][0], runs["graph", "hip"][0]
+    assert np.all(np.abs(lf[:2] - lh[:2]) <= 1e-5 * np.abs(lf[:2])), (lf, lh)
+
+
+def test_hip_adam_matches_torch_adam(dev):
+    """HipAdam (clip_grad_value_ + Adam in one nerf_adam_step launch) against
+    torch.optim.Adam (foreach=False) after torch's clip_grad_value_, 6 steps on
+    tensors of the network's sizes with gradients past the clip value: the
+    parameters, exp_avg and exp_avg_sq within 1e-5 of each tensor's max (the
+    same float32 operation order; torch's device lerp may contract to an fma,
+    one ulp that the moving averages carry on), the clamped gradients and the
+    step count exact; an lr
+    change through the device tensor takes effect; state_dict round trip."""
+    from nerfhip.adam import HipAdam
+    g = torch.Generator(device=dev).manual_seed(5)
+    shapes = [(256, 63), (256,), (256, 256), (1,), (3, 128), (3,), (128, 283), (128,)]
+    p0 = [torch.randn(s, device=dev, generator=g) for s in shapes]
+    pa = [x.clone().requires_grad_(True) for x in p0]
+    pb = [x.clone().requires_grad_(True) for x in p0]
+    oa = HipAdam(pa, lr=5e-3, eps=1e-8, clip=40.0)
+    ob = torch.optim.Adam(pb, lr=5e-3, eps=1e-8, weight_decay=0.0, foreach=False)
+    for step in range(6):
+        if step == 4:
+            oa.param_groups[0]["lr"].fill_(1e-3)
+            ob.param_groups[0]["lr"] = 1e-3
+        for a, b in zip(pa, pb):
+            gr = torch.randn(a.shape, device=dev, generator=g) * 30.0
+            a.grad, b.grad = gr.clone(), gr.clone()
+        torch.nn.utils.clip_grad_value_(pb, 40.0)
+        oa.step()
+        ob.step()
+        for a, b in zip(pa, pb):
+            assert torch.equal(a.grad, b.grad)
+            assert (a - b).abs().max() <= 1e-5 * b.abs().max(), step
+            sa, sb = oa.state[a], ob.state[b]
+            for k in ("exp_avg", "exp_avg_sq"):
+                assert (sa[k] - sb[k]).abs().max() <= 1e-5 * sb[k].abs().max(), (step, k)
+            assert float(sa["step"]) == float(sb["step"]) == step + 1
+    sd = oa.state_dict()
+    oc = HipAdam([x.detach().clone().requires_grad_(True) for x in pa], lr=1e-3, clip=40.0)
+    oc.load_state_dict(sd)
+    for x in oc.param_groups[0]["params"]:
+        x.grad = torch.zeros_like(x)
+    oc.step()
+    assert float(oc.state[oc.param_groups[0]["params"][0]]["step"]) == 7.0

@@ -224,6 +224,17 @@ def test_freq_encode_fm_matches_torch(dev, P, L):
     xr = x.clone().requires_grad_(True)
     (gr,) = torch.autograd.grad(freq_encode(xr, L), xr, d_enc.t())
     assert _rel(dx, gr) < 1e-5
+    # the training backward's form: two gradient row sets summed in the kernel,
+    # sin / cos read from the forward's rows (out, padded to the same stride)
+    d_a = _act(F, P, dev)
+    d_b = _act(F, P, dev)
+    d_a.copy_(d_enc * 0.25)
+    d_b.copy_(d_enc * 0.75)
+    dx2 = torch.empty((P, 3), device=dev)
+    call("nerf_freq_encode_fm_backward_sum", ptr(d_a), ptr(d_b), d_a.stride(0), ptr(out),
+         ptr(x), 3, P, L, ptr(dx2), _lib.stream_of(dev))
+    (gr2,) = torch.autograd.grad(freq_encode(xr, L), xr, (d_a + d_b).t())
+    assert _rel(dx2, gr2) < 1e-5
 
 
 def test_x3_train_mlp_denormal_sample_gradients(dev):
