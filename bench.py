@@ -126,10 +126,20 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
               file=sys.stderr)
+    # NERF_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N > 1 path
+    # (every collective, barrier and max-over-ranks of the timed region) on a
+    # one-GPU box, ranks sharing the device; the driver's runs use RCCL ("nccl"),
+    # one rank per GPU.
+    backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     H, W = args.H, args.W
     ckpt = args.checkpoint
