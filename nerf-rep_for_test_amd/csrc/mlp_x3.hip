@@ -425,7 +425,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, 
 // indices. Otherwise the samples are 0 .. total.
 // TRACE (diagnostic twin only): the first lane of workgroups 0..3 stamps
 // s_memtime at each of its first 32 tiles' start, after the tile's sample
-// loads + encoding, and at its end: trace[(b * 32 + i) * 4 + 0..2].
+// loads + encoding, and at its end: trace[(b * 32 + i) * 4 + 0..2]; [3]: after
+// the loads, before the encoding.
 template <bool LIST, bool TRAIN, bool TRACE = false>
 __device__ __forceinline__ void mlp_x3_body(
     const float4* __restrict__ slices, const float* __restrict__ head,
@@ -481,6 +482,10 @@ __device__ __forceinline__ void mlp_x3_body(
   for (int c = 0; c < 3; ++c) {
     dv[c] = rays_d[ray * 3 + c];
     p[c] = rays_o[ray * 3 + c] + dv[c] * zv;      // VR:165: o + d*z, two roundings
+  }
+  if constexpr (TRACE) {   // the sample inputs have landed (before the encoding)
+    asm volatile("" ::"v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(dv[0]), "v"(dv[1]), "v"(dv[2]));
+    if (tr) trp[3] = __builtin_amdgcn_s_memtime();
   }
   Op encf[2];                   // FP32 encoding (split in place for the skip layer)
   encode_xyz(p, g4, encf);

@@ -43,7 +43,8 @@ def main(reps=5):
         t = trace.view(-1, 4).cpu().numpy().astype(np.float64)
         t = t[(t[:, 2] > t[:, 0]) & (t[:, 1] >= t[:, 0])]
         print(f"run {r}: clock {ghz:.3f} GHz, tile {np.median(t[:, 2] - t[:, 0]):.0f} cycles, "
-              f"start share {np.median((t[:, 1] - t[:, 0]) / (t[:, 2] - t[:, 0])):.4f}, "
+              f"start share {np.median((t[:, 1] - t[:, 0]) / (t[:, 2] - t[:, 0])):.4f} "
+              f"(loads {np.median((t[:, 3] - t[:, 0]) / (t[:, 2] - t[:, 0])):.4f}), "
               f"launch {np.median(c[:, 1] - c[:, 0]) / ghz / 1e3:.1f} us (median workgroup)",
               flush=True)
 
