@@ -404,15 +404,28 @@ __global__ void kn_at_b_kernel(const float* __restrict__ A, int64_t ac, const fl
 // summation-order bound 2 n u sum|terms| (tests/test_gpu_kilonerf.py).
 // ---------------------------------------------------------------------------
 typedef float kn_f32x4 __attribute__((ext_vector_type(4)));
-constexpr int GG_ROWS = 64;                // rows per workgroup: 4 waves x 16
+constexpr int GG_ROWS = 128;               // rows per workgroup: 4 waves x 32 (two 16-row tiles)
 constexpr int GG_MAX_IN = 120;             // K (padded to 4) held in LDS
-constexpr int GG_MAX_OUT = 64;             // N (padded to 16): 4 accumulator tiles per wave
-__host__ __device__ __forceinline__ int gg_wstride(int np) { return np % 32 == 0 ? np + 16 : np; }
+constexpr int GG_MAX_OUT = 64;             // N (padded to 16): 4 accumulator tiles per row tile
+// LDS row strides, bank-conflict-free for the MFMA operand reads (ds_read_b32:
+// bank (a/4) mod 32 over each 32-lane half = 2 K rows x 16 lanes): W rows
+// (k0 + kq) * ws + l16 need ws = 16 mod 32; X rows (r0 + l16) * xs + kq need
+// xs = 2 mod 32.
+__host__ __device__ __forceinline__ int gg_wstride(int np) { return np + ((16 - np % 32) + 32) % 32; }
+__host__ __device__ __forceinline__ int gg_xstride(int kp) { return kp + ((2 - kp % 32) + 32) % 32; }
+__host__ __device__ __forceinline__ size_t gg_lds_bytes(int in_f, int out_f) {
+  const int kp = (in_f + 3) & ~3, np = (out_f + 15) & ~15;
+  const int xr = gg_xstride(kp) > out_f ? gg_xstride(kp) : out_f;   // X tile, then the output tile
+  return (size_t)(kp * gg_wstride(np) + GG_ROWS * xr) * sizeof(float);
+}
 
-// out[r] = X[r] . W_net (+ bias_net), rows of network net0 + blockIdx.y, 64 per
-// workgroup (blockIdx.x). W_net and the X tile (one contiguous run of rows)
-// are staged in LDS; wave w owns tile rows 16w .. 16w+15: A = X (16 rows x 4
-// k), B = W (4 k x 16 columns), one accumulator per 16-column tile.
+// out[r] = X[r] . W_net (+ bias_net), rows of network net0 + blockIdx.y, 128 per
+// workgroup (blockIdx.x). W_net and the X tile (one contiguous run of nrow *
+// in_f floats) are staged in LDS, the X rows by whole-row coalesced loads
+// (eight rows per wave in flight); wave w owns tile rows 32w .. 32w+31: A = X
+// (16 rows x 4 k), B = W (4 k x 16 columns), one accumulator per (row tile,
+// 16-column tile). The output tile is staged back through LDS (the X region)
+// and written as one contiguous run of nrow * out_f floats.
 __global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
     int mode, const float* __restrict__ bias, const float* __restrict__ X,
     const float* __restrict__ W, int out_f, int in_f, float* __restrict__ out, SegBatch sb,
@@ -424,9 +437,41 @@ __global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
   if (t0 >= rows) return;   // block-uniform
   const int net = net0 + k;
   const int kp = (in_f + 3) & ~3, np = (out_f + 15) & ~15;
-  const int ws = gg_wstride(np), xs = kp + 1;   // LDS row strides
+  const int ws = gg_wstride(np), xs = gg_xstride(kp);
   float* Ws = gg_sm;                            // [kp][ws]
-  float* Xs = gg_sm + kp * ws;                  // [64][xs]
+  float* Xs = gg_sm + kp * ws;                  // [128][xs]; then the output tile [nrow][out_f]
+                                                // (gg_lds_bytes sizes the region for both)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nrow = (int)(rows - t0 < GG_ROWS ? rows - t0 : GG_ROWS);
+  const float* x = X + (r0 + t0) * in_f;        // nrow * in_f contiguous floats
+  // X rows first (the long-latency part), 8 rows per wave in flight; K padding
+  // columns zero (W's padding rows are zero too, but LDS garbage may be NaN);
+  // rows >= nrow are left as they are: they only reach output rows never stored.
+  // (Issuing all of a workgroup's W and X loads before any LDS store measured
+  // slower: 0.547 vs 0.453 ms, 139 VGPRs.)
+  for (int rb = wave; rb < nrow; rb += 32) {
+    float v[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + 4 * u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kk = lane + 64 * h;
+        v[u][h] = (r < nrow && kk < in_f) ? x[(int64_t)r * in_f + kk] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + 4 * u;
+      if (r < nrow) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int kk = lane + 64 * h;
+          if (kk < kp) Xs[r * xs + kk] = v[u][h];
+        }
+      }
+    }
+  }
   const float* w = W + (int64_t)net * out_f * in_f;
   for (int i = threadIdx.x; i < kp * np; i += 256) {
     const int kk = i / np, c = i - kk * np;
@@ -434,52 +479,68 @@ __global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
     if (kk < in_f && c < out_f) v = mode == 2 ? w[(int64_t)c * in_f + kk] : w[(int64_t)kk * out_f + c];
     Ws[kk * ws + c] = v;
   }
-  const int64_t nrow = rows - t0 < GG_ROWS ? rows - t0 : GG_ROWS;
-  const float* x = X + (r0 + t0) * in_f;   // nrow * in_f contiguous floats
-  for (int i = threadIdx.x; i < GG_ROWS * kp; i += 256) {
-    const int rr = i / kp, kk = i - rr * kp;
-    Xs[rr * xs + kk] = (rr < nrow && kk < in_f) ? x[(int64_t)rr * in_f + kk] : 0.0f;
-  }
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kq = lane >> 4, l16 = lane & 15;
   const int nt = np / 16;
-  kn_f32x4 acc[GG_MAX_OUT / 16];
+  kn_f32x4 acc[2][GG_MAX_OUT / 16];
 #pragma unroll
-  for (int c = 0; c < GG_MAX_OUT / 16; ++c) acc[c] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* xa = Xs + (wave * 16 + l16) * xs + kq;
-  const float* wb = Ws + kq * ws + l16;
-  for (int k0 = 0; k0 < kp; k0 += 4) {
-    const float a = xa[k0];
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int c = 0; c < GG_MAX_OUT / 16; ++c)
-      if (c < nt) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[k0 * ws + 16 * c], acc[c], 0, 0, 0);
+    for (int c = 0; c < GG_MAX_OUT / 16; ++c) acc[t][c] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool busy = wave * 32 < nrow;   // wave-uniform
+  if (busy) {
+    const float* xa = Xs + (wave * 32 + l16) * xs + kq;
+    const float* wb = Ws + kq * ws + l16;
+    for (int k0 = 0; k0 < kp; k0 += 4) {
+      const float a0 = xa[k0], a1 = xa[16 * xs + k0];
+#pragma unroll
+      for (int c = 0; c < GG_MAX_OUT / 16; ++c)
+        if (c < nt) {
+          const float b = wb[k0 * ws + 16 * c];
+          acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][c], 0, 0, 0);
+          acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][c], 0, 0, 0);
+        }
+    }
   }
-  // lane holds rows 4 kq + i, column l16 of each 16-column tile
+  __syncthreads();   // every wave is done with Xs: it now holds the output tile
+  float* Os = Xs;    // [nrow][out_f], dense
+  if (busy) {
+    // lane holds rows 4 kq + i of each row tile, column l16 of each 16-column tile
 #pragma unroll
-  for (int c = 0; c < GG_MAX_OUT / 16; ++c) {
-    const int col = 16 * c + l16;
-    if (c < nt && col < out_f) {
-      const float bb = mode == 0 ? bias[(int64_t)net * out_f + col] : 0.0f;
+    for (int c = 0; c < GG_MAX_OUT / 16; ++c) {
+      const int col = 16 * c + l16;
+      if (c < nt && col < out_f) {
+        const float bb = mode == 0 ? bias[(int64_t)net * out_f + col] : 0.0f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = wave * 16 + 4 * kq + i;
-        if (rr < nrow) out[(r0 + t0 + rr) * out_f + col] = mode == 0 ? acc[c][i] + bb : acc[c][i];
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rr = wave * 32 + 16 * t + 4 * kq + i;
+            if (rr < nrow) Os[rr * out_f + col] = mode == 0 ? acc[t][c][i] + bb : acc[t][c][i];
+          }
       }
     }
   }
+  __syncthreads();
+  float* o = out + (r0 + t0) * out_f;
+  const int n = nrow * out_f;
+  for (int i = threadIdx.x; i < n; i += 256) o[i] = Os[i];
 }
 
-constexpr int AB_MAX_T = 4;   // 16-wide tiles per side (a_cols, b_cols <= 64)
+constexpr int AB_MAX_T = 4;     // 16-wide tiles per side (a_cols, b_cols <= 64)
+constexpr int AB_WAVES = 8;     // waves per network
+constexpr int AB_UNROLL = 4;    // row quads per wave whose loads are in flight together
+                                // (8: 0.252 vs 0.214 ms at 4096 networks)
 
 // out_net = A_net^T B_net ([ac][bc]) over the network's rows, one workgroup
-// per network: wave w takes row quads w, w+4, ...; A operand = A^T (16 a x
-// 4 rows), B operand = B (4 rows x 16 b); the 4 waves' partial tiles are
-// summed in LDS in wave order.
-__global__ __launch_bounds__(256) void kn_at_b_mfma_kernel(const float* __restrict__ A, int ac,
-                                                           const float* __restrict__ B, int bc,
-                                                           float* __restrict__ out, SegBatch sb,
-                                                           int net0) {
+// per network: wave w takes row quads w, w + 8, ...; A operand = A^T (16 a x
+// 4 rows), B operand = B (4 rows x 16 b). The loads of AB_UNROLL row quads are
+// issued before their MFMAs (a network's ~256 rows are a few such batches, so
+// the kernel is bound by how many loads are in flight, not by the MFMAs); the
+// 8 waves' partial tiles are summed in LDS in wave order.
+__global__ __launch_bounds__(64 * AB_WAVES) void kn_at_b_mfma_kernel(
+    const float* __restrict__ A, int ac, const float* __restrict__ B, int bc,
+    float* __restrict__ out, SegBatch sb, int net0) {
   extern __shared__ float ab_sm[];
   const int k = blockIdx.x;
   const int64_t r0 = sb.off[k], r1 = sb.off[k + 1];
@@ -491,21 +552,28 @@ __global__ __launch_bounds__(256) void kn_at_b_mfma_kernel(const float* __restri
   for (int i = 0; i < AB_MAX_T; ++i)
 #pragma unroll
     for (int j = 0; j < AB_MAX_T; ++j) acc[i][j] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t rb = r0 + 4 * wave; rb < r1; rb += 16) {
-    const int64_t r = rb + kq;
-    const bool ok = r < r1;
-    float a[AB_MAX_T], b[AB_MAX_T];
+  constexpr int kStep = 4 * AB_WAVES;
+  for (int64_t rb = r0 + 4 * wave; rb < r1; rb += (int64_t)kStep * AB_UNROLL) {
+    float a[AB_UNROLL][AB_MAX_T], b[AB_UNROLL][AB_MAX_T];
 #pragma unroll
-    for (int i = 0; i < AB_MAX_T; ++i) {
-      const int ca = 16 * i + l16, cb = 16 * i + l16;
-      a[i] = (i < ta && ok && ca < ac) ? A[r * ac + ca] : 0.0f;
-      b[i] = (i < tb && ok && cb < bc) ? B[r * bc + cb] : 0.0f;
+    for (int u = 0; u < AB_UNROLL; ++u) {
+      const int64_t r = rb + (int64_t)kStep * u + kq;
+      const bool ok = r < r1;
+#pragma unroll
+      for (int i = 0; i < AB_MAX_T; ++i) {
+        const int c = 16 * i + l16;
+        a[u][i] = (i < ta && ok && c < ac) ? A[r * ac + c] : 0.0f;
+        b[u][i] = (i < tb && ok && c < bc) ? B[r * bc + c] : 0.0f;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < AB_MAX_T; ++i)
+    for (int u = 0; u < AB_UNROLL; ++u)
 #pragma unroll
-      for (int j = 0; j < AB_MAX_T; ++j)
-        if (i < ta && j < tb) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < AB_MAX_T; ++i)
+#pragma unroll
+        for (int j = 0; j < AB_MAX_T; ++j)
+          if (i < ta && j < tb)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
   }
   // partial tile (i, j) of wave w at ab_sm[((w * ta + i) * tb + j) * 256 + 64 * e + lane]
 #pragma unroll
@@ -518,13 +586,13 @@ __global__ __launch_bounds__(256) void kn_at_b_mfma_kernel(const float* __restri
   __syncthreads();
   const int per = ta * tb * 256;
   float* o = out + (int64_t)(net0 + k) * ac * bc;
-  for (int idx = threadIdx.x; idx < per; idx += 256) {
+  for (int idx = threadIdx.x; idx < per; idx += 64 * AB_WAVES) {
     const int tile = idx >> 8, e = (idx >> 6) & 3, ln = idx & 63;
     const int i = tile / tb, j = tile - i * tb;
     const int ra = 16 * i + 4 * (ln >> 4) + e, cbx = 16 * j + (ln & 15);
     if (ra < ac && cbx < bc) {
       float s = ab_sm[idx];
-      for (int w = 1; w < 4; ++w) s = s + ab_sm[w * per + idx];
+      for (int w = 1; w < AB_WAVES; ++w) s = s + ab_sm[w * per + idx];
       o[(int64_t)ra * bc + cbx] = s;
     }
   }
@@ -903,8 +971,7 @@ int kn_multimatmul_grouped(int handle, int mode, const float* biases, const floa
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t mr) {
     if (mr == 0) return 0;
     if (in_f <= GG_MAX_IN && out_f <= GG_MAX_OUT) {
-      const int kp = ((int)in_f + 3) & ~3, np = ((int)out_f + 15) & ~15;
-      const size_t lds = (size_t)(kp * gg_wstride(np) + GG_ROWS * (kp + 1)) * sizeof(float);
+      const size_t lds = gg_lds_bytes((int)in_f, (int)out_f);
       hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel, dim3((unsigned)cdiv(mr, GG_ROWS), sb.count),
                          dim3(256), lds, as_stream(stream), mode, biases, X, W, (int)out_f,
                          (int)in_f, out, sb, net0);
@@ -935,8 +1002,8 @@ int kn_multimatmul_A_transposed(const float* A, int64_t a_cols, const float* B, 
                "kn_multimatmul_A_transposed: bad argument");
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t) {
     if (a_cols <= 16 * AB_MAX_T && b_cols <= 16 * AB_MAX_T) {
-      const size_t lds = 4 * cdiv(a_cols, 16) * cdiv(b_cols, 16) * 256 * sizeof(float);
-      hipLaunchKernelGGL(kn_at_b_mfma_kernel, dim3((unsigned)sb.count), dim3(256), lds,
+      const size_t lds = AB_WAVES * cdiv(a_cols, 16) * cdiv(b_cols, 16) * 256 * sizeof(float);
+      hipLaunchKernelGGL(kn_at_b_mfma_kernel, dim3((unsigned)sb.count), dim3(64 * AB_WAVES), lds,
                          as_stream(stream), A, (int)a_cols, B, (int)b_cols, out, sb, net0);
       return check_launch("kn_at_b_mfma_kernel");
     }
