@@ -28,6 +28,9 @@ using namespace nerfhip;
 #ifndef SPREAD
 #define SPREAD 0
 #endif
+#ifndef SPLITW
+#define SPLITW 0   // 1: counted lgkmcnt waits at each fragment's first MFMA (NS = 1 only)
+#endif
 
 constexpr int kSl = 64;   // slices per tile (8 layers x 8 K steps)
 
@@ -44,7 +47,14 @@ template <int G, int NS, int Q>
 __device__ __forceinline__ void grp(St<NS>& st, unsigned base, unsigned nbase, Frags& x, Frags& y,
                                     const Dma& dma) {
   if constexpr (G < 8) {
+#if SPLITW
+    // wait for each fragment right before its first MFMA (LDS reads return in
+    // order): h0, then l0, h1, l1 with the next group's 4 reads behind them
+    asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#else
     lds_drain();
+#endif
     if constexpr (G + 1 < 8) {
       if constexpr ((G & 1) == 0) load_frags<G + 1>(y, base);
       else load_frags<G + 1>(x, base);
@@ -52,11 +62,33 @@ __device__ __forceinline__ void grp(St<NS>& st, unsigned base, unsigned nbase, F
       load_frags<0>(x, nbase);
     }
     __builtin_amdgcn_sched_barrier(0);
+#if SPLITW
+    static_assert(NS == 1, "SPLITW: one sample group");
+    {
+      const Frags& f = (G & 1) ? y : x;
+      f32x4& c0 = st.acc[0][2 * G];
+      f32x4& c1 = st.acc[0][2 * G + 1];
+      const half8 bh = op_hi(st.X[0][Q]), bl = op_lo(st.X[0][Q]);
+      c0 = MFMA16(f.h0, bh, Q == 0 ? f32x4(0.0f) : c0);
+      c0 = MFMA16(f.h0, bl, c0);
+      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      c0 = MFMA16(f.l0, bh, c0);
+      asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      c1 = MFMA16(f.h1, bh, Q == 0 ? f32x4(0.0f) : c1);
+      c1 = MFMA16(f.h1, bl, c1);
+      asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      c1 = MFMA16(f.l1, bh, c1);
+    }
+#else
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       if constexpr ((G & 1) == 0) mfma3x2<Q == 0>(st.acc[n][2 * G], st.acc[n][2 * G + 1], x, st.X[n][Q]);
       else mfma3x2<Q == 0>(st.acc[n][2 * G], st.acc[n][2 * G + 1], y, st.X[n][Q]);
     }
+#endif
     if constexpr (Q < 7) {   // split of operand Q+1, values G, G+1 (even G)
       if constexpr ((G & 1) == 0) {
 #pragma unroll
@@ -212,7 +244,7 @@ double run(const float4* dw, float* dout, int grid, int samples, hipEvent_t e0, 
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   const double flop = (double)tiles * per * kSl * 256.0 * 32 * 2 * 3;
-  printf("WPS=%d NS=%d SPREAD=%d samples=%d: %.3f ms  %.1f TF/s  frac %.4f\n", WPS, NS, SPREAD,
+  printf("SPLITW=%d WPS=%d NS=%d SPREAD=%d samples=%d: %.3f ms  %.1f TF/s  frac %.4f\n", SPLITW, WPS, NS, SPREAD,
          tiles * per, ms, flop / ms / 1e9, flop / ms / 1e9 / 2516.8);
   return ms;
 }
@@ -237,8 +269,10 @@ int main(int argc, char** argv) {
   const int grid = prop.multiProcessorCount;
   for (int rep = 0; rep < 3; ++rep) {
     run<2, 1>(dw, dout, grid, samples, e0, e1);
+#if !SPLITW
     run<1, 2>(dw, dout, grid, samples, e0, e1);
     run<1, 3>(dw, dout, grid, samples, e0, e1);
+#endif
   }
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) { printf("error %s\n", hipGetErrorString(err)); return 1; }
