@@ -119,6 +119,8 @@ def _order_bound(terms_abs, n):
     (32, 63, [0, 3, 130, 1, 64, 0, 200]),              # MFMA kernel (KiloNeRF first layer)
     (3, 32, [17, 0, 300, 5]),                          # rgb head: one padded column tile
     (64, 120, [65, 1, 129]),                           # largest MFMA shapes, ragged tiles
+    (64, 32, [127, 128, 129, 256, 0, 300]),            # output tile wider than the X tile
+                                                       # (staged in the X region), 128-row edges
     (20, 130, [40, 0, 7])])                            # beyond the LDS budget: fallback kernel
 def test_multimatmul_grouped(kn, mode, out_f, in_f, bspn):
     """multimatmul.cu:244-361 vs the sequential restatement; MAGMA's own
