@@ -145,10 +145,12 @@ def test_multimatmul_grouped(kn, mode, out_f, in_f, bspn):
 
 
 @pytest.mark.parametrize("ac,bc,bspn", [(32, 7, [4, 0, 33, 100]), (32, 63, [1, 517, 0, 64]),
-                                        (3, 64, [2000, 9]), (65, 7, [30, 3])])
+                                        (3, 64, [2000, 9]), (64, 64, [31, 257, 1100]),
+                                        (65, 7, [30, 3])])
 def test_row_sum_and_A_transposed(kn, ac, bc, bspn):
     """multimatmul.cu:560-623 (row sums and A^T B per network) within the
-    summation-order bound; (65, 7) exceeds the MFMA tile budget (fallback)."""
+    summation-order bound; (64, 64) is the largest MFMA shape (128 KiB of wave
+    partials in LDS); (65, 7) exceeds the MFMA tile budget (fallback)."""
     rng = np.random.default_rng(ac * bc)
     M = rng.normal(size=(sum(bspn), 33)).astype(np.float32)
     out = kn.multi_row_sum_reduction(cu(M), torch.tensor(bspn)).cpu().numpy()
