@@ -1620,19 +1620,26 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 
 
 // The same partial weight gradients for aligned operands (host-checked: P a
-// multiple of 32, 16-B aligned rows, operands < 2 GiB): the raw FP32 K steps
-// land in LDS by buffer-form LDS-DMA, so no registers hold in-flight data and
-// step k+1's 64 KiB (A and B rows of 32 samples) stream in during all of step
-// k's work; each wave splits the fragments it reads (FP32 -> FP16 hi/lo) in
-// registers. LDS: 2 stages x 64 pieces of 1 KiB; piece (o, t, h) = operand o
-// (A, B), 16-row tile t, half h: lane l holds row 16t + (l & 15), samples
-// 8 (l >> 4) + 4h .. +3, so the two halves read by lane l are one MFMA
-// fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past M / N read 0
-// (offset past num_records). Bias sums from the A fragments (waves nb = 0).
-// The body for output tile (mtile, ntile) and K subset z of Z; subset z's
-// partials go to part + z * ldpart ([M][N]) and bias_part + z * ldbias ([M]).
+// multiple of 32, 16-B rows, operands < 2 GiB): the raw FP32 K steps land in
+// LDS by buffer-form LDS-DMA, so no registers hold in-flight data; each wave
+// splits the fragments it reads (FP32 -> FP16 hi/lo) in registers. A K step
+// (32 samples) is two granules of 32 KiB, A_k (256 rows of A) then B_k, and
+// the granules stream through a 5-slot ring (160 KiB, all of the CU's LDS):
+// while step k is multiplied, B_{k+1}, A_{k+1} and A_{k+2} are landing. A
+// wave's 8 LDS-DMA pieces of a step (4 of B_{k+1}, then 4 of A_{k+2}) are
+// issued one per B tile of its MFMA loop, so their issue cost overlaps the
+// MFMAs (issued all at once after the step's barrier, every wave of the CU
+// stalled on them together with the MFMA pipes idle).
+// Piece (t, h) of a granule = 16-row tile t, half h: lane l holds row
+// 16t + (l & 15), samples 8 (l >> 4) + 4h .. +3, so the two halves read by
+// lane l are one MFMA fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past
+// M / N read 0 (offset past num_records). Bias sums from the A fragments
+// (waves nb = 0). The body for output tile (mtile, ntile) and K subset z of Z;
+// subset z's partials go to part + z * ldpart ([M][N]) and bias_part + z *
+// ldbias ([M]).
+constexpr int kWgRing = 5;
 __device__ __forceinline__ void wgrad_dma_body(
-    uint4 (&stg)[2][64 * 64], const float* __restrict__ A, int64_t lda, int M,
+    uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float* __restrict__ amax_a,
     const float* __restrict__ amax_b, float* __restrict__ part, int64_t ldpart,
     float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z) {
@@ -1641,29 +1648,38 @@ __device__ __forceinline__ void wgrad_dma_body(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
   const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
   const int64_t pb = (int64_t)z * 32, kstride = (int64_t)Z * 32;
+  const int nsteps = pb < P ? (int)((P - pb + kstride - 1) / kstride) : 0;
+  const int ngran = 2 * nsteps;
   const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
 
-  // this wave's 8 pieces per step: q = 8 wave + i (waves 0-3: A, 4-7: B)
-  const bool opb = wave >= 4;
+  // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1)
   const int nbA = (int)((int64_t)M * lda * 4), nbB = (int)((int64_t)N * ldb * 4);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(opb ? B : A), 0, opb ? nbB : nbA, 0x00020000);
-  unsigned vo[8];
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nbA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
+  unsigned voA[4], voB[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int q = (8 * wave + i) & 31, t = q >> 1, h = q & 1;
-    const int row = (opb ? n0 : m0) + 16 * t + (lane & 15);
-    const int64_t ld = opb ? ldb : lda;
-    vo[i] = row < (opb ? N : M) ? (unsigned)(((int64_t)row * ld + 8 * (lane >> 4) + 4 * h) * 4)
-                               : (unsigned)(opb ? nbB : nbA);
+  for (int i = 0; i < 4; ++i) {
+    const int q = 4 * wave + i, t = q >> 1, h = q & 1;
+    const int col = 8 * (lane >> 4) + 4 * h;
+    const int ra = m0 + 16 * t + (lane & 15), rb = n0 + 16 * t + (lane & 15);
+    voA[i] = ra < M ? (unsigned)(((int64_t)ra * lda + col) * 4) : (unsigned)nbA;
+    voB[i] = rb < N ? (unsigned)(((int64_t)rb * ldb + col) * 4) : (unsigned)nbB;
   }
-  auto issue = [&](int64_t k, int s) {
-    const int so = __builtin_amdgcn_readfirstlane((int)(k * 4));
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(&stg[s][(8 * wave + i) * 64]), 16,
-                                               (int)vo[i], so, 0, 0);
+  // piece I of granule g: A (g even) or B (g odd) of step g >> 1, into slot g % 5
+  auto issue_piece = [&](int g, auto Ic) {
+    constexpr int I = decltype(Ic)::value;
+    if (g >= ngran) return;
+    const int so = __builtin_amdgcn_readfirstlane((int)((pb + (int64_t)(g >> 1) * kstride) * 4));
+    uint4* dst = &ring[g % kWgRing][(4 * wave + I) * 64];
+    if (g & 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_ptr_t)dst, 16, (int)voB[I], so, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)dst, 16, (int)voA[I], so, 0, 0);
+  };
+  auto issue = [&](int g) {
+    issue_piece(g, std::integral_constant<int, 0>{});
+    issue_piece(g, std::integral_constant<int, 1>{});
+    issue_piece(g, std::integral_constant<int, 2>{});
+    issue_piece(g, std::integral_constant<int, 3>{});
   };
 
   const int mb = wave & 3, nb = wave >> 2;   // wave tile: rows 64 mb.., cols 128 nb..
@@ -1675,7 +1691,7 @@ __device__ __forceinline__ void wgrad_dma_body(
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.0f);
   float rs4[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's share of sum_p A (nb = 0)
 
-  // the raw FP32 fragment of a tile: its two pieces (halves), 2 KiB apart per tile
+  // the raw FP32 fragment of a tile: its two pieces (halves), 1 KiB apart
   // Raw: the two halves as the asm wrote them. A drain names every pending Raw
   // as an in/out operand, so no copy or shuffle of one can run before it lands.
   struct Raw { u32x4 x, y; };
@@ -1687,56 +1703,73 @@ __device__ __forceinline__ void wgrad_dma_body(
     return __builtin_bit_cast(Op, __builtin_shufflevector(r.x, r.y, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
-  if (pb < P) issue(pb, 0);
-  int s = 0;
-  for (int64_t k0 = pb; k0 < P; k0 += kstride, s ^= 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of step k0
-    __builtin_amdgcn_s_barrier();   // everyone's landed; stage s^1's readers are done
+  // prologue: granules 0 .. 2 (A_0, B_0, A_1)
+  for (int g = 0; g < 3 && g < ngran; ++g) issue(g);
+  for (int k = 0; k < nsteps; ++k) {
+    // granules <= 2k+1 landed (this wave's pieces); 2k+2 (4 pieces) may stay in flight
+    if (2 * k + 2 < ngran) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // everyone's landed; slots of step k-1 are free
     asm volatile("" ::: "memory");
-    if (k0 + kstride < P) issue(k0 + kstride, s ^ 1);
-    if (busy) {
-      const unsigned base = lds_addr((const float*)&stg[s][0]) + lane * 16u;
-      half8 ah[4], al[4];
-      {
-        Raw ra[4];
+    const int gb = 2 * k + 3, ga = 2 * k + 4;   // B_{k+1}, A_{k+2}: issued during this step
+    if (!busy) {   // nothing to multiply: stage this wave's pieces at once
+      issue(gb);
+      issue(ga);
+      continue;
+    }
+    const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
+    const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
+    half8 ah[4], al[4];
+    {
+      Raw ra[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) read_pair(base + (unsigned)((4 * mb + i) * 2048), ra[i]);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
-                       "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y)
-                     :
-                     : "memory");
+      for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
+                     "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y)
+                   :
+                   : "memory");
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          Op v = to_op(ra[i]);
-          if (nb == 0) {
+      for (int i = 0; i < 4; ++i) {
+        Op v = to_op(ra[i]);
+        if (nb == 0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) rs4[i] += v[j];
-          }
-          split_op(v, sa);
-          ah[i] = op_hi(v);
-          al[i] = op_lo(v);
+          for (int j = 0; j < 8; ++j) rs4[i] += v[j];
         }
-      }
-      Raw rb[2];
-      // B tile nt = 8 nb + j: pieces 32 + 2 nt, + 1
-      read_pair(base + (unsigned)((16 + 8 * nb) * 2048), rb[0]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Raw& cur = rb[j & 1];
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
-        Op b = to_op(cur);
-        if (j + 1 < 8) read_pair(base + (unsigned)((16 + 8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
-        split_op(b, sb);
-        const half8 bh = op_hi(b), bl = op_lo(b);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
-          acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
-          acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
-        }
+        split_op(v, sa);
+        ah[i] = op_hi(v);
+        al[i] = op_lo(v);
       }
     }
+    Raw rb[2];
+    // B tile nt = 8 nb + j
+    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);
+    auto tile = [&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      Raw& cur = rb[j & 1];
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
+      Op b = to_op(cur);
+      if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
+      // one LDS-DMA piece per B tile: B_{k+1} pieces 0-3, then A_{k+2} pieces 0-3
+      if constexpr (j < 4) issue_piece(gb, std::integral_constant<int, j>{});
+      else issue_piece(ga, std::integral_constant<int, j - 4>{});
+      split_op(b, sb);
+      const half8 bh = op_hi(b), bl = op_lo(b);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
+        acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
+        acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
+      }
+    };
+    tile(std::integral_constant<int, 0>{});
+    tile(std::integral_constant<int, 1>{});
+    tile(std::integral_constant<int, 2>{});
+    tile(std::integral_constant<int, 3>{});
+    tile(std::integral_constant<int, 4>{});
+    tile(std::integral_constant<int, 5>{});
+    tile(std::integral_constant<int, 6>{});
+    tile(std::integral_constant<int, 7>{});
   }
   if (bias_part && ntile == 0 && nb == 0 && busy) {
 #pragma unroll
@@ -1768,8 +1801,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
     const float* __restrict__ A, int64_t lda, int M, const float* __restrict__ B, int64_t ldb,
     int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
     float* __restrict__ part, float* __restrict__ bias_part) {
-  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
-  wgrad_dma_body(stg, A, lda, M, B, ldb, N, P, amax_a, amax_b, part, (int64_t)M * N, bias_part,
+  __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
+  wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, amax_a, amax_b, part, (int64_t)M * N, bias_part,
                  M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z);
 }
 
@@ -1791,7 +1824,7 @@ struct WgradBatch {
 };
 
 __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const WgradBatch bt) {
-  __shared__ __attribute__((aligned(16))) uint4 stg[2][64 * 64];
+  __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
   const int w = (int)blockIdx.x;
   int t = 0;
   while (t + 1 < bt.nt && w >= bt.t_wg_end[t]) ++t;
@@ -1799,7 +1832,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
   const int z = w - (bt.t_wg_end[t] - Z);
   const NerfWgradDesc& d = bt.d[bt.t_desc[t]];
   const int mtile = bt.t_m[t], ntile = bt.t_n[t];
-  wgrad_dma_body(stg, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, d.amax_a, d.amax_b, d.part,
+  wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, d.amax_a, d.amax_b, d.part,
                  d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z);
   if (z != 0 || Z >= bt.Zmax) return;
   // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)
