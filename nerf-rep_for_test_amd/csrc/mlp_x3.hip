@@ -1719,35 +1719,26 @@ __device__ __forceinline__ void wgrad_dma_body(
     }
     const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
     const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
+    // The A fragments and the first B fragment are read together; the A split
+    // runs tile by tile inside the first B tile's MFMAs (each A tile split just
+    // before its own three products), so it is not a VALU-only phase at the
+    // start of every step.
     half8 ah[4], al[4];
-    {
-      Raw ra[4];
+    Raw ra[4], rb[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
-                     "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y)
-                   :
-                   : "memory");
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        Op v = to_op(ra[i]);
-        if (nb == 0) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) rs4[i] += v[j];
-        }
-        split_op(v, sa);
-        ah[i] = op_hi(v);
-        al[i] = op_lo(v);
-      }
-    }
-    Raw rb[2];
+    for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
     // B tile nt = 8 nb + j
     read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
+                   "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y),
+                   "+v"(rb[0].x), "+v"(rb[0].y)
+                 :
+                 : "memory");
     auto tile = [&](auto Jc) {
       constexpr int j = decltype(Jc)::value;
       Raw& cur = rb[j & 1];
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
+      if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
       Op b = to_op(cur);
       if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
       // one LDS-DMA piece per B tile: B_{k+1} pieces 0-3, then A_{k+2} pieces 0-3
@@ -1757,6 +1748,16 @@ __device__ __forceinline__ void wgrad_dma_body(
       const half8 bh = op_hi(b), bl = op_lo(b);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if constexpr (j == 0) {
+          Op v = to_op(ra[i]);
+          if (nb == 0) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) rs4[i] += v[t];
+          }
+          split_op(v, sa);
+          ah[i] = op_hi(v);
+          al[i] = op_lo(v);
+        }
         acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
         acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
         acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
