@@ -411,73 +411,63 @@ constexpr int GG_MAX_OUT = 64;             // N (padded to 16): 4 accumulator ti
 // bank (a/4) mod 32 over each 32-lane half = 2 K rows x 16 lanes): W rows
 // (k0 + kq) * ws + l16 need ws = 16 mod 32; X rows (r0 + l16) * xs + kq need
 // xs = 2 mod 32.
-__host__ __device__ __forceinline__ int gg_wstride(int np) { return np + ((16 - np % 32) + 32) % 32; }
-__host__ __device__ __forceinline__ int gg_xstride(int kp) { return kp + ((2 - kp % 32) + 32) % 32; }
+// LDS image (floats): W_net as stored (mode 0/1: [in_f][out_f], mode 2:
+// [out_f][in_f]) rounded up to whole 64-float LDS-DMA pieces, then the X tile
+// as stored ([128][in_f] dense), whose region the output tile ([nrow][out_f]
+// dense) reuses.
+__host__ __device__ __forceinline__ int gg_wfloats(int in_f, int out_f) {
+  return (in_f * out_f + 63) & ~63;
+}
 __host__ __device__ __forceinline__ size_t gg_lds_bytes(int in_f, int out_f) {
-  const int kp = (in_f + 3) & ~3, np = (out_f + 15) & ~15;
-  const int xr = gg_xstride(kp) > out_f ? gg_xstride(kp) : out_f;   // X tile, then the output tile
-  return (size_t)(kp * gg_wstride(np) + GG_ROWS * xr) * sizeof(float);
+  return (size_t)(gg_wfloats(in_f, out_f) + GG_ROWS * (in_f > out_f ? in_f : out_f)) * sizeof(float);
 }
 
 // out[r] = X[r] . W_net (+ bias_net), rows of network net0 + blockIdx.y, 128 per
 // workgroup (blockIdx.x). W_net and the X tile (one contiguous run of nrow *
-// in_f floats) are staged in LDS, the X rows by whole-row coalesced loads
-// (eight rows per wave in flight); wave w owns tile rows 32w .. 32w+31: A = X
-// (16 rows x 4 k), B = W (4 k x 16 columns), one accumulator per (row tile,
-// 16-column tile). The output tile is staged back through LDS (the X region)
-// and written as one contiguous run of nrow * out_f floats.
+// in_f floats) land in LDS by buffer-form LDS-DMA (4 B per lane, 64-float
+// pieces, reads past either run return 0): every load of the workgroup is in
+// flight at once and no register holds staged data (register staging with one
+// load -> store trip per row batch measured 0.45 ms at 4096 networks, a
+// chain of HBM latencies per workgroup). Wave w owns tile rows 32w .. 32w+31:
+// A = X (16 rows x 4 k), B = W (4 k x 16 columns), one accumulator per (row
+// tile, 16-column tile); K and column padding are zeroed in registers. The
+// output tile is staged back through LDS (the X region) and written as one
+// contiguous run of nrow * out_f floats.
+// Row offsets of the networks: a kernel-argument batch (SegBatch, at most
+// SEG_BATCH networks per launch) or a device array (a grouped-GEMM handle's
+// buffer: every network in one launch).
+__device__ __forceinline__ int64_t off_at(const SegBatch& sb, int k) { return sb.off[k]; }
+__device__ __forceinline__ int64_t off_at(const int64_t* off, int k) { return off[k]; }
+
+template <typename Off>
 __global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
     int mode, const float* __restrict__ bias, const float* __restrict__ X,
-    const float* __restrict__ W, int out_f, int in_f, float* __restrict__ out, SegBatch sb,
+    const float* __restrict__ W, int out_f, int in_f, float* __restrict__ out, Off sb,
     int net0) {
   extern __shared__ float gg_sm[];
   const int k = blockIdx.y;
-  const int64_t r0 = sb.off[k], rows = sb.off[k + 1] - r0;
+  const int64_t r0 = off_at(sb, k), rows = off_at(sb, k + 1) - r0;
   const int64_t t0 = (int64_t)blockIdx.x * GG_ROWS;
   if (t0 >= rows) return;   // block-uniform
   const int net = net0 + k;
   const int kp = (in_f + 3) & ~3, np = (out_f + 15) & ~15;
-  const int ws = gg_wstride(np), xs = gg_xstride(kp);
-  float* Ws = gg_sm;                            // [kp][ws]
-  float* Xs = gg_sm + kp * ws;                  // [128][xs]; then the output tile [nrow][out_f]
-                                                // (gg_lds_bytes sizes the region for both)
+  float* Ws = gg_sm;                               // W_net as stored
+  float* Xs = gg_sm + gg_wfloats(in_f, out_f);     // [128][in_f]; then the output tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nrow = (int)(rows - t0 < GG_ROWS ? rows - t0 : GG_ROWS);
-  const float* x = X + (r0 + t0) * in_f;        // nrow * in_f contiguous floats
-  // X rows first (the long-latency part), 8 rows per wave in flight; K padding
-  // columns zero (W's padding rows are zero too, but LDS garbage may be NaN);
-  // rows >= nrow are left as they are: they only reach output rows never stored.
-  // (Issuing all of a workgroup's W and X loads before any LDS store measured
-  // slower: 0.547 vs 0.453 ms, 139 VGPRs.)
-  for (int rb = wave; rb < nrow; rb += 32) {
-    float v[8][2];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = rb + 4 * u;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int kk = lane + 64 * h;
-        v[u][h] = (r < nrow && kk < in_f) ? x[(int64_t)r * in_f + kk] : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = rb + 4 * u;
-      if (r < nrow) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int kk = lane + 64 * h;
-          if (kk < kp) Xs[r * xs + kk] = v[u][h];
-        }
-      }
-    }
-  }
-  const float* w = W + (int64_t)net * out_f * in_f;
-  for (int i = threadIdx.x; i < kp * np; i += 256) {
-    const int kk = i / np, c = i - kk * np;
-    float v = 0.0f;
-    if (kk < in_f && c < out_f) v = mode == 2 ? w[(int64_t)c * in_f + kk] : w[(int64_t)kk * out_f + c];
-    Ws[kk * ws + c] = v;
+  {
+    const int nx = nrow * in_f, nw = in_f * out_f;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(X + (r0 + t0) * in_f), 0, nx * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(W + (int64_t)net * nw), 0, nw * 4, 0x00020000);
+    for (int p = wave; p < (nx + 63) / 64; p += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(Xs + 64 * p),
+                                               4, (p * 64 + lane) * 4, 0, 0, 0);
+    for (int p = wave; p < (nw + 63) / 64; p += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(Ws + 64 * p),
+                                               4, (p * 64 + lane) * 4, 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   const int kq = lane >> 4, l16 = lane & 15;
@@ -489,14 +479,18 @@ __global__ __launch_bounds__(256) void kn_grouped_gemm_mfma_kernel(
     for (int c = 0; c < GG_MAX_OUT / 16; ++c) acc[t][c] = kn_f32x4{0.f, 0.f, 0.f, 0.f};
   const bool busy = wave * 32 < nrow;   // wave-uniform
   if (busy) {
-    const float* xa = Xs + (wave * 32 + l16) * xs + kq;
-    const float* wb = Ws + kq * ws + l16;
+    // rows >= nrow read whatever the LDS holds: they only reach output rows that
+    // are never stored
+    const float* xa = Xs + (wave * 32 + l16) * in_f + kq;
+    const int cstride = mode == 2 ? in_f : 1, kstride = mode == 2 ? 1 : out_f;
+    const float* wb = Ws + kq * kstride + l16 * cstride;
     for (int k0 = 0; k0 < kp; k0 += 4) {
-      const float a0 = xa[k0], a1 = xa[16 * xs + k0];
+      const bool kok = k0 + kq < in_f;
+      const float a0 = kok ? xa[k0] : 0.0f, a1 = kok ? xa[16 * in_f + k0] : 0.0f;
 #pragma unroll
       for (int c = 0; c < GG_MAX_OUT / 16; ++c)
         if (c < nt) {
-          const float b = wb[k0 * ws + 16 * c];
+          const float b = (kok && 16 * c + l16 < out_f) ? wb[k0 * kstride + 16 * c * cstride] : 0.0f;
           acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][c], 0, 0, 0);
           acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][c], 0, 0, 0);
         }
@@ -746,6 +740,7 @@ __global__ __launch_bounds__(256) void kn_network_eval_kernel(
 struct GemmHandle {
   int64_t num_networks, out_f, in_f;
   std::vector<int> group_limits;
+  int64_t* d_off = nullptr;   // device row offsets [num_networks + 1], rewritten per call
 };
 
 static std::mutex g_mu;
@@ -946,6 +941,13 @@ int kn_init_multimatmul_grouped(int64_t num_networks, int64_t out_f, int64_t in_
   std::lock_guard<std::mutex> lk(g_mu);
   GemmHandle hd{num_networks, out_f, in_f, {}};
   for (int i = 0; i < n_group_limits; ++i) hd.group_limits.push_back(group_limits[i]);
+  if (num_networks > 0 && num_networks <= 65535) {   // grid.y bound of the one-launch path
+    // without the buffer (no device, out of memory) calls take the batched launches
+    if (hipMalloc(&hd.d_off, (size_t)(num_networks + 1) * sizeof(int64_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      hd.d_off = nullptr;
+    }
+  }
   *handle = g_gemm_next++;
   g_gemm[*handle] = hd;
   return 0;
@@ -953,26 +955,63 @@ int kn_init_multimatmul_grouped(int64_t num_networks, int64_t out_f, int64_t in_
 
 int kn_deinit_multimatmul_grouped(int handle) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_gemm.erase(handle)) return fail(NERF_E_HANDLE, "kn_deinit_multimatmul_grouped: unknown handle");
+  auto it = g_gemm.find(handle);
+  if (it == g_gemm.end()) return fail(NERF_E_HANDLE, "kn_deinit_multimatmul_grouped: unknown handle");
+  // a launch may still read the offsets: free them once the device is done
+  if (it->second.d_off) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(it->second.d_off);
+  }
+  g_gemm.erase(it);
   return 0;
 }
 
 int kn_multimatmul_grouped(int handle, int mode, const float* biases, const float* X,
                            const float* W, int64_t out_f, int64_t in_f, const int64_t* bspn,
                            int num_networks, float* out, nerf_stream_t stream) {
+  int64_t* d_off = nullptr;
+  int64_t hnets = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_gemm.count(handle)) return fail(NERF_E_HANDLE, "kn_multimatmul_grouped: unknown handle");
+    auto it = g_gemm.find(handle);
+    if (it == g_gemm.end()) return fail(NERF_E_HANDLE, "kn_multimatmul_grouped: unknown handle");
+    d_off = it->second.d_off;
+    hnets = it->second.num_networks;
   }
   NERF_REQUIRE(X && W && out && bspn && (mode != 0 || biases) && mode >= 0 && mode <= 2,
                "kn_multimatmul_grouped: bad argument");
   NERF_REQUIRE(out_f > 0 && in_f > 0 && out_f < (1 << 20) && in_f < (1 << 20),
                "kn_multimatmul_grouped: bad feature sizes");
+  if (d_off && num_networks >= 1 && num_networks <= hnets && in_f <= GG_MAX_IN &&
+      out_f <= GG_MAX_OUT) {
+    // every network in ONE launch: the row offsets go to the handle's device
+    // buffer (stream-ordered copy from a temporary host array: the runtime
+    // stages pageable memory before hipMemcpyAsync returns; a handle serves one
+    // stream at a time, as the reference's MAGMA queues do)
+    std::vector<int64_t> off((size_t)num_networks + 1);
+    int64_t row = 0, maxrows = 0;
+    for (int k = 0; k < num_networks; ++k) {
+      if (bspn[k] < 0) return fail(NERF_E_ARG, "negative batch_size_per_network entry");
+      off[k] = row;
+      row += bspn[k];
+      maxrows = bspn[k] > maxrows ? bspn[k] : maxrows;
+    }
+    off[num_networks] = row;
+    if (maxrows == 0) return 0;
+    const hipError_t e = hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(int64_t),
+                                        hipMemcpyHostToDevice, as_stream(stream));
+    if (e != hipSuccess) return fail((int)e, "kn_multimatmul_grouped: offset upload failed");
+    hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel<const int64_t*>,
+                       dim3((unsigned)cdiv(maxrows, GG_ROWS), (unsigned)num_networks), dim3(256),
+                       gg_lds_bytes((int)in_f, (int)out_f), as_stream(stream), mode, biases, X, W,
+                       (int)out_f, (int)in_f, out, (const int64_t*)d_off, 0);
+    return check_launch("kn_grouped_gemm_mfma_kernel");
+  }
   return for_each_segment_batch(bspn, num_networks, [&](const SegBatch& sb, int net0, int64_t mr) {
     if (mr == 0) return 0;
     if (in_f <= GG_MAX_IN && out_f <= GG_MAX_OUT) {
       const size_t lds = gg_lds_bytes((int)in_f, (int)out_f);
-      hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel, dim3((unsigned)cdiv(mr, GG_ROWS), sb.count),
+      hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel<SegBatch>, dim3((unsigned)cdiv(mr, GG_ROWS), sb.count),
                          dim3(256), lds, as_stream(stream), mode, biases, X, W, (int)out_f,
                          (int)in_f, out, sb, net0);
       return check_launch("kn_grouped_gemm_mfma_kernel");
