@@ -432,7 +432,11 @@ int kn_init_magma(void);
  *   mode 0 (static, with bias) / 1 (without bias): W_k stored [in_f][out_f];
  *   mode 2 (without bias, transposed weights):     W_k stored [out_f][in_f].
  * bias: [num_networks][out_f] (mode 0 only). batch_size_per_network is HOST
- * memory (the reference reads it on the host). Handle = returned by init. */
+ * memory (the reference reads it on the host). Handle = returned by init; it
+ * owns a device buffer of num_networks + 1 row offsets, rewritten by each call
+ * (stream-ordered), so one handle serves one stream at a time, as the
+ * reference's per-handle MAGMA state does. deinit synchronises the device
+ * before freeing it. */
 int kn_init_multimatmul_grouped(int64_t num_networks, int64_t out_features, int64_t in_features,
                                 const int32_t* group_limits, int n_group_limits, int* handle);
 int kn_deinit_multimatmul_grouped(int handle);
