@@ -31,6 +31,12 @@ using namespace nerfhip;
 #ifndef SPLITW
 #define SPLITW 0   // 1: counted lgkmcnt waits at each fragment's first MFMA (NS = 1 only)
 #endif
+#ifndef LOADHI
+#define LOADHI 0   // 1: waves 4-7 stage the weights (the shipped kernel: waves 0-3)
+#endif
+#ifndef PRIO
+#define PRIO 0     // 1: s_setprio 1 on the waves that do not stage weights
+#endif
 
 constexpr int kSl = 64;   // slices per tile (8 layers x 8 K steps)
 
@@ -171,7 +177,7 @@ __device__ __forceinline__ void slice(St<NS>& st, float* ring, const float4* w, 
   float* nbuf = ring + ((g + 1) & 3) * kSliceFloats;
   const int t = g + 3;
   const Dma d = make_dma_blocks(w, t % kSl, ring + (t & 3) * kSliceFloats, (wave & 3) * 8, wave,
-                                lane, wave < 4, kSl);
+                                lane, LOADHI ? wave >= 4 : wave < 4, kSl);
   grp<0, NS, Q>(st, lds_base(buf, lane), lds_base(nbuf, lane), x, y, d);
   if constexpr (Q == 7) epi_last(st);
   slice_end<1, 8>();
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256 * WPS, 1) void ns_kernel(const float4* __restri
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int t = 0; t < 3; ++t) {
     const Dma d = make_dma_blocks(w, t, ring + t * kSliceFloats, (wave & 3) * 8, wave, lane,
-                                  wave < 4, kSl);
+                                  LOADHI ? wave >= 4 : wave < 4, kSl);
     if (d.live) {
       stage_piece<0>(d); stage_piece<1>(d); stage_piece<2>(d); stage_piece<3>(d);
       stage_piece<4>(d); stage_piece<5>(d); stage_piece<6>(d); stage_piece<7>(d);
@@ -193,6 +199,9 @@ __global__ __launch_bounds__(256 * WPS, 1) void ns_kernel(const float4* __restri
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#if PRIO
+  if (LOADHI ? wave < 4 : wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   St<NS> st;
   float osum = 0.0f;
   int g = 0;
@@ -244,7 +253,7 @@ double run(const float4* dw, float* dout, int grid, int samples, hipEvent_t e0, 
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   const double flop = (double)tiles * per * kSl * 256.0 * 32 * 2 * 3;
-  printf("SPLITW=%d WPS=%d NS=%d SPREAD=%d samples=%d: %.3f ms  %.1f TF/s  frac %.4f\n", SPLITW, WPS, NS, SPREAD,
+  printf("LOADHI=%d PRIO=%d SPLITW=%d WPS=%d NS=%d SPREAD=%d samples=%d: %.3f ms  %.1f TF/s  frac %.4f\n", LOADHI, PRIO, SPLITW, WPS, NS, SPREAD,
          tiles * per, ms, flop / ms / 1e9, flop / ms / 1e9 / 2516.8);
   return ms;
 }
@@ -269,7 +278,7 @@ int main(int argc, char** argv) {
   const int grid = prop.multiProcessorCount;
   for (int rep = 0; rep < 3; ++rep) {
     run<2, 1>(dw, dout, grid, samples, e0, e1);
-#if !SPLITW
+#if !SPLITW && !LOADHI && !PRIO
     run<1, 2>(dw, dout, grid, samples, e0, e1);
     run<1, 3>(dw, dout, grid, samples, e0, e1);
 #endif
