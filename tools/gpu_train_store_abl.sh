@@ -1,3 +1,11 @@
+#!/bin/bash
+# Timing-only ablation of the fused training forward's activation stores
+# (tools/time_train_fwd.py) against two libraries built from temporary patches
+# of csrc/mlp_x3.hip (not kept in the tree): libnerfhip_nostore.so, whose
+# ActStore::pair returns at once (no stores), and libnerfhip_zerorec.so, whose
+# rows_rsrc gives zero-record descriptors (stores issued, dropped by the range
+# check). Build each with the Makefile's flags from the patched file and link
+# it with the other objects of build/.
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
