@@ -92,6 +92,8 @@ def main():
                     help="synthetic generator weights even when the trained checkpoint exists")
     ap.add_argument("--no-gt", action="store_true",
                     help="skip the PSNR/SSIM-vs-ground-truth renders (profiling runs)")
+    ap.add_argument("--no-perturb", action="store_true",
+                    help="skip the perturb-1 eval timing reported under 'c2_perturb'")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 train-step sub-record of the default run")
     ap.add_argument("--train-mlp", default="x3", choices=["x3", "torch"],
@@ -116,7 +118,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from nerfhip.dist import render_frame_interleaved, render_frame_sharded
+    from nerfhip import _lib
     from nerfhip.render import NerfPipeline
     from nerfhip.synthetic import make_occupancy_grid, make_params
 
@@ -173,21 +175,13 @@ def main():
             pipe.set_grid(make_occupancy_grid(0, 128, 1.2, 0.1))
         return pipe
 
-    def frame_fn(pipe, ess_ert):
-        """One sharded frame: C2 row bands; C4 2048-ray chunks dealt round-robin
-        (chunk c -> rank c mod P), grid self-updates replayed."""
-        def frame(pose, K):
-            if ess_ert:
-                return render_frame_interleaved(
-                    lambda cs: pipe.render_chunks(H, W, pose, K, cs), H, W, rank, world, dev)
-            return render_frame_sharded(lambda p0, n: pipe.render_band(H, W, pose, K, p0, n),
-                                        H, W, rank, world, dev)
-        return frame
+    def frame_fn(pipe, ess_ert, perturb=False):
+        return make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb)
 
-    def measure(precision, ess_ert, steps, warmup):
+    def measure(precision, ess_ert, steps, warmup, perturb=False):
         """warmup + K timed frames (barrier + sync both sides, max over ranks)."""
         pipe = make_pipe(precision, ess_ert)
-        frame = frame_fn(pipe, ess_ert)
+        frame = frame_fn(pipe, ess_ert, perturb)
         for i in range(warmup):
             frame(*lego_camera(H, W, i))
         torch.cuda.synchronize()
@@ -209,9 +203,9 @@ def main():
         timer, pipe.timer = pipe.timer, None
         stages, pipe.stage_timer = pipe.stage_timer, None
         roof = roofline(precision, timer, elapsed, world, H, W,
-                        pmc_workload=world == 1 and not ess_ert)
+                        pmc_workload=world == 1 and not ess_ert and not perturb)
         roof["byte_kernels"] = byte_kernels(stages, steps)
-        if precision == "f16x3" and not ess_ert:
+        if precision == "f16x3" and not ess_ert and not perturb:
             roof.update(held_clock(pipe, H, W, roof["achieved"], roof["peak"]))
         return pipe, elapsed, roof
 
@@ -244,6 +238,7 @@ def main():
                                    f"c mod {world}) + RCCL all-gather of pixels" if c4 else
                                    f"row-band tiles x{world} + RCCL all-gather of pixels")},
         "roofline": roof,
+        "build_id": _lib.build_id(),
     }
     if c4:
         result["ert_compaction"] = ert_report(pipe, rays, world, args.ert_segment, dev)
@@ -304,6 +299,25 @@ def main():
                 p4, "r2_c4_frame16", H, W, ckpt)
             del p4
         result["c4_ess_ert"] = rec
+    if args.config == "c2" and not args.no_perturb:
+        # what `run.py --type evaluate` with lego.yaml runs: perturb 1 at eval
+        # (lego.yaml:22, VR:228-235), per-ray jittered coarse depths
+        torch.cuda.empty_cache()
+        pp_steps = max(1, min(args.steps, 5))
+        _, elp, roofp = measure(args.precision, False, pp_steps, 1, perturb=True)
+        raysp = H * W * pp_steps
+        result["c2_perturb"] = {
+            "metric": "Mrays/s + ms/frame, lego 800x800 (64c+128f), perturb 1 at eval",
+            "value": raysp / elp / 1e6, "unit": "Mrays/s", "steps": pp_steps, "warmup": 1,
+            "ms_per_step": elp / pp_steps * 1e3, "dtype": DTYPES[args.precision],
+            "config": {"workload": "lego 800x800, 64c+128f, ESS/ERT off, perturb 1 (the "
+                                   "stratified jitter drawn on the device per band inside the "
+                                   "frame, one [n, 64] uniform draw), eval-mode fine u, 1 frame "
+                                   "per step (test poses cycled)",
+                       "baseline_config": "configs[1] as run.py --type evaluate renders it",
+                       "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
+            "roofline": {k: roofp[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
+                                               "avg_launch_ms", "launches", "mlp_share_of_step")}}
     if world == 1 and args.config == "c2" and not args.no_c3:
         # the frames' multi-GB buffers are still cached by torch's allocator: give
         # them back before the 1024-ray step settles into its own working set
@@ -320,6 +334,35 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb=False):
+    """One sharded frame (frame(pose, K) -> the assembled maps on every rank):
+    C2 row bands; C4 2048-ray chunks dealt round-robin (chunk c -> rank c mod P,
+    SURVEY §8e), grid self-updates replayed. perturb: the reference's eval-mode
+    stratified jitter (perturb 1, lego.yaml:22; VR:228-235), one [n, 64] uniform
+    draw per band on the device (torch's Philox) inside the frame, so the coarse
+    pass reads per-ray depth rows. tests/test_gpu_dist.py drives this same
+    function from two processes."""
+    from nerfhip.dist import render_frame_interleaved, render_frame_sharded
+    import torch
+
+    def band(pose, K):
+        def render(p0, n):
+            if not perturb:
+                return pipe.render_band(H, W, pose, K, p0, n)
+            if n == 0:
+                return {}
+            tr = torch.rand((n, pipe.N_samples), device=dev)
+            return pipe.render_image(H, W, pose, K, t_rand=tr, p0=p0, n=n)
+        return render
+
+    def frame(pose, K):
+        if ess_ert:
+            return render_frame_interleaved(
+                lambda cs: pipe.render_chunks(H, W, pose, K, cs), H, W, rank, world, dev)
+        return render_frame_sharded(band(pose, K), H, W, rank, world, dev)
+    return frame
 
 
 def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmup=None,
@@ -412,6 +455,7 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
                    "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
         "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
+        "build_id": __import__("nerfhip._lib", fromlist=["build_id"]).build_id(),
     }
     if not emit:
         return result

@@ -37,6 +37,11 @@ enum {
 
 const char* nerf_last_error(void);
 int nerf_version(void);                 /* ABI version, bumped on layout changes */
+/* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
+ * source tree this library was compiled from (nerfhip/_lib.py refuses a
+ * library whose id differs from the tree beside it; the reference's
+ * counterpart is its extension build, cuda/setup.py:13-24). */
+const char* nerf_build_id(void);
 
 /* ---------------------------------------------------------------------------
  * 1. Render path

@@ -741,6 +741,8 @@ struct GemmHandle {
   int64_t num_networks, out_f, in_f;
   std::vector<int> group_limits;
   int64_t* d_off = nullptr;   // device row offsets [num_networks + 1], rewritten per call
+  int64_t* h_off = nullptr;   // pinned staging of the offsets (the copy reads it async)
+  hipEvent_t staged = nullptr;  // the last upload from h_off: h_off is reused after it
 };
 
 static std::mutex g_mu;
@@ -941,11 +943,24 @@ int kn_init_multimatmul_grouped(int64_t num_networks, int64_t out_f, int64_t in_
   std::lock_guard<std::mutex> lk(g_mu);
   GemmHandle hd{num_networks, out_f, in_f, {}};
   for (int i = 0; i < n_group_limits; ++i) hd.group_limits.push_back(group_limits[i]);
-  if (num_networks > 0 && num_networks <= 65535) {   // grid.y bound of the one-launch path
-    // without the buffer (no device, out of memory) calls take the batched launches
-    if (hipMalloc(&hd.d_off, (size_t)(num_networks + 1) * sizeof(int64_t)) != hipSuccess) {
+  int dev = 0, max_y = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&max_y, hipDeviceAttributeMaxGridDimY, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    max_y = 0;
+  }
+  if (num_networks > 0 && num_networks <= max_y) {   // grid.y bound of the one-launch path
+    // without the buffers (no device, out of memory) calls take the batched launches
+    const size_t nb = (size_t)(num_networks + 1) * sizeof(int64_t);
+    if (hipMalloc(&hd.d_off, nb) != hipSuccess ||
+        hipHostMalloc((void**)&hd.h_off, nb, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&hd.staged, hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
+      if (hd.d_off) (void)hipFree(hd.d_off);
+      if (hd.h_off) (void)hipHostFree(hd.h_off);
       hd.d_off = nullptr;
+      hd.h_off = nullptr;
+      hd.staged = nullptr;
     }
   }
   *handle = g_gemm_next++;
@@ -961,6 +976,8 @@ int kn_deinit_multimatmul_grouped(int handle) {
   if (it->second.d_off) {
     (void)hipDeviceSynchronize();
     (void)hipFree(it->second.d_off);
+    (void)hipHostFree(it->second.h_off);
+    (void)hipEventDestroy(it->second.staged);
   }
   g_gemm.erase(it);
   return 0;
@@ -970,14 +987,26 @@ int kn_multimatmul_grouped(int handle, int mode, const float* biases, const floa
                            const float* W, int64_t out_f, int64_t in_f, const int64_t* bspn,
                            int num_networks, float* out, nerf_stream_t stream) {
   int64_t* d_off = nullptr;
+  int64_t* h_off = nullptr;
+  hipEvent_t staged = nullptr;
   int64_t hnets = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_gemm.find(handle);
     if (it == g_gemm.end()) return fail(NERF_E_HANDLE, "kn_multimatmul_grouped: unknown handle");
     d_off = it->second.d_off;
+    h_off = it->second.h_off;
+    staged = it->second.staged;
     hnets = it->second.num_networks;
   }
+  // a captured graph would replay the upload of one call's offsets: take the
+  // batched launches (offsets as kernel arguments) while the stream captures
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(as_stream(stream), &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    cap = hipStreamCaptureStatusActive;
+  }
+  if (cap != hipStreamCaptureStatusNone) d_off = nullptr;
   NERF_REQUIRE(X && W && out && bspn && (mode != 0 || biases) && mode >= 0 && mode <= 2,
                "kn_multimatmul_grouped: bad argument");
   NERF_REQUIRE(out_f > 0 && in_f > 0 && out_f < (1 << 20) && in_f < (1 << 20),
@@ -985,21 +1014,27 @@ int kn_multimatmul_grouped(int handle, int mode, const float* biases, const floa
   if (d_off && num_networks >= 1 && num_networks <= hnets && in_f <= GG_MAX_IN &&
       out_f <= GG_MAX_OUT) {
     // every network in ONE launch: the row offsets go to the handle's device
-    // buffer (stream-ordered copy from a temporary host array: the runtime
-    // stages pageable memory before hipMemcpyAsync returns; a handle serves one
-    // stream at a time, as the reference's MAGMA queues do)
-    std::vector<int64_t> off((size_t)num_networks + 1);
+    // buffer by a stream-ordered copy from its pinned staging array, which is
+    // rewritten only once the previous call's copy has read it (a handle serves
+    // one stream at a time, as the reference's MAGMA queues do)
     int64_t row = 0, maxrows = 0;
     for (int k = 0; k < num_networks; ++k) {
       if (bspn[k] < 0) return fail(NERF_E_ARG, "negative batch_size_per_network entry");
-      off[k] = row;
       row += bspn[k];
       maxrows = bspn[k] > maxrows ? bspn[k] : maxrows;
     }
-    off[num_networks] = row;
     if (maxrows == 0) return 0;
-    const hipError_t e = hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(int64_t),
-                                        hipMemcpyHostToDevice, as_stream(stream));
+    hipError_t e = hipEventSynchronize(staged);
+    if (e != hipSuccess) return fail((int)e, "kn_multimatmul_grouped: staging wait failed");
+    row = 0;
+    for (int k = 0; k < num_networks; ++k) {
+      h_off[k] = row;
+      row += bspn[k];
+    }
+    h_off[num_networks] = row;
+    e = hipMemcpyAsync(d_off, h_off, (size_t)(num_networks + 1) * sizeof(int64_t),
+                       hipMemcpyHostToDevice, as_stream(stream));
+    if (e == hipSuccess) e = hipEventRecord(staged, as_stream(stream));
     if (e != hipSuccess) return fail((int)e, "kn_multimatmul_grouped: offset upload failed");
     hipLaunchKernelGGL(kn_grouped_gemm_mfma_kernel<const int64_t*>,
                        dim3((unsigned)cdiv(maxrows, GG_ROWS), (unsigned)num_networks), dim3(256),

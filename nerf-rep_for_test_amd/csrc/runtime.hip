@@ -29,4 +29,9 @@ const char* nerf_last_error(void) { return nerfhip::g_last_error.c_str(); }
 
 int nerf_version(void) { return 1; }
 
+#ifndef NERF_BUILD_ID
+#define NERF_BUILD_ID "unknown"
+#endif
+const char* nerf_build_id(void) { return NERF_BUILD_ID; }
+
 }  // extern "C"

@@ -489,8 +489,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const floa
     const int64_t i = base + r * 256 + threadIdx.x;
     if (i < T.n) {
       float g = T.g[i];
-      if (clip > 0.0f) {
-        g = fminf(fmaxf(g, -clip), clip);
+      if (clip >= 0.0f) {   // torch.clamp keeps a NaN (fminf/fmaxf would drop it)
+        g = (g != g) ? g : fminf(fmaxf(g, -clip), clip);
         T.g[i] = g;
       }
       const float m0 = T.m[i];

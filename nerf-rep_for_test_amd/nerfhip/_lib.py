@@ -22,6 +22,7 @@ _P, _I, _I64, _F, _S, _SZ = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_void_
 SIGNATURES = {
     "nerf_last_error": (C.c_char_p, []),
     "nerf_version": (_I, []),
+    "nerf_build_id": (C.c_char_p, []),
     "nerf_rays": (_I, [_P, _I, _I, _I64, _I64, _P, _P, _S]),
     "nerf_sample_coarse": (_I, [_P, _P, _I64, _I, _P, _S]),
     "nerf_mlp_forward": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I, _P, _S]),
@@ -86,8 +87,34 @@ class NerfHipError(RuntimeError):
     pass
 
 
+def tree_build_id():
+    """sha256 (16 hex digits) of the csrc/ files in byte order, then
+    include/nerfhip.h -- the digest the Makefile bakes into the library as
+    nerf_build_id(); None when the sources are not beside the package."""
+    import hashlib
+    src = os.path.join(PKG_ROOT, "csrc")
+    hdr = os.path.join(os.path.dirname(PKG_ROOT), "include", "nerfhip.h")
+    if not (os.path.isdir(src) and os.path.exists(hdr)):
+        return None
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(src)):
+        fp = os.path.join(src, f)
+        if os.path.isfile(fp):
+            with open(fp, "rb") as fh:
+                h.update(fh.read())
+    with open(hdr, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    """The source-tree digest compiled into the loaded library."""
+    return lib().nerf_build_id().decode()
+
+
 def lib():
-    """Load the library once (raises NerfHipError if it is not built)."""
+    """Load the library once (raises NerfHipError if it is not built, or if it was
+    built from sources other than the tree beside it: the measured binary is HEAD's)."""
     global _lib
     with _lock:
         if _lib is None:
@@ -100,6 +127,14 @@ def lib():
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args
+            want = tree_build_id()
+            got = h.nerf_build_id().decode()
+            # NERFHIP_LIB points at a deliberately different build (timing-only
+            # variants of tools/): its id is reported, not enforced
+            if want is not None and got != want and "NERFHIP_LIB" not in os.environ:
+                raise NerfHipError(
+                    f"{LIB_PATH} was built from sources with id {got}, but the tree holds "
+                    f"{want}: rebuild with `make -C nerf-rep_for_test_amd`")
             _lib = h
     return _lib
 

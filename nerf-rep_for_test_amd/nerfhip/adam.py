@@ -27,10 +27,16 @@ class _AdamTensor(ctypes.Structure):
 
 class HipAdam(torch.optim.Adam):
     """Adam (weight decay 0, no amsgrad) + gradient value clipping at ``clip``
-    (<= 0: none; the gradients are clamped in place, as clip_grad_value_ does),
-    one parameter group, float32 contiguous parameters on one ROCm device."""
+    (None: none; any clip >= 0 clamps the gradients in place to [-clip, clip]
+    as clip_grad_value_ does, NaN kept), one parameter group, float32
+    contiguous parameters on one ROCm device.
 
-    def __init__(self, params, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, clip=0.0):
+    One step count serves every parameter (it lives on the device for graph
+    capture), so every parameter must have a gradient at every step (torch's
+    Adam would skip one without and keep a separate count): ``step`` raises
+    otherwise, and a loaded state dict must hold one common step value."""
+
+    def __init__(self, params, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, clip=None):
         params = list(params)
         dev = params[0].device
         if dev.type != "cuda":
@@ -40,7 +46,9 @@ class HipAdam(torch.optim.Adam):
                          foreach=False)
         if len(self.param_groups) != 1:
             raise ValueError("HipAdam takes one parameter group")
-        self.clip = float(clip)
+        if clip is not None and not clip >= 0:
+            raise ValueError("HipAdam: clip must be None (no clipping) or >= 0")
+        self.clip = -1.0 if clip is None else float(clip)   # < 0 tells the kernel: none
         self._count = torch.zeros(1, device=dev, dtype=torch.float32)   # shared step count
         self._done = torch.zeros(1, device=dev, dtype=torch.int32)     # finished workgroups
         self._key = None
@@ -53,7 +61,13 @@ class HipAdam(torch.optim.Adam):
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
         elif st["step"].data_ptr() != self._count.data_ptr():
-            # a loaded state dict: every parameter was stepped together
+            # a loaded state dict: every parameter must have been stepped together
+            steps = {float(self.state[q]["step"]) for q in self.param_groups[0]["params"]
+                     if q in self.state and "step" in self.state[q]
+                     and self.state[q]["step"].data_ptr() != self._count.data_ptr()}
+            if len(steps) > 1:
+                raise ValueError(f"HipAdam: loaded state holds different step counts {steps}; "
+                                 "it keeps one count for all parameters")
             self._count.copy_(st["step"].reshape(1).to(self._count))
             st["step"] = self._count.view(())
         return st
@@ -69,6 +83,10 @@ class HipAdam(torch.optim.Adam):
         if not torch.is_tensor(lr):   # a float lr set by someone else: back on the device
             lr = g["lr"] = torch.tensor(float(lr), device=self._count.device)
         rows = []
+        missing = [p for p in g["params"] if p.grad is None]
+        if missing and len(missing) != len(g["params"]):
+            raise ValueError(f"HipAdam: {len(missing)} of {len(g['params'])} parameters have no "
+                             "gradient; its shared step count needs all of them every step")
         for p in g["params"]:
             if p.grad is None:
                 continue

@@ -24,6 +24,8 @@ ops, no host sync): packing order = ``pack_x3_matrix``.
 """
 from __future__ import annotations
 
+import functools
+
 import ctypes
 import os as _os
 
@@ -544,6 +546,13 @@ WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "512"))
 
 
 def wgrad_tile_chunks(shapes, P, n_cu=256, floor=None):
+    """Memoised (the search repeats every backward with the same arguments)."""
+    return list(_wgrad_tile_chunks(tuple(tuple(int(v) for v in s) for s in shapes), int(P),
+                                   int(n_cu), floor))
+
+
+@functools.lru_cache(maxsize=64)
+def _wgrad_tile_chunks(shapes, P, n_cu, floor):
     """K split of every 256 x 256 output tile of a batched weight-gradient
     launch (order: descriptor, N tile, M tile): proportional to the operand
     rows the tile streams per K step (A rows + B rows, at least 128: a step

@@ -35,6 +35,18 @@ reference's source is stored - only numbers it produced.
     python tests/golden/make_ref_frames.py            # all frames (~20 min, 8 threads)
     python tests/golden/make_ref_frames.py r0_c2_frame0
     python tests/golden/make_ref_frames.py --add-gt   # store the GT PNG in older files
+    python tests/golden/make_ref_frames.py --zall     # zh_<name>.npz, see below
+
+``--zall`` renders each frame again (asserting every map equals the stored
+one) and writes ``tests/golden/zh_<name>.npz``: the reference's disp maps
+(``disp_map``, ``disp_map_0``, VR:333, NaN where acc = 0), the fine depths
+the fine composite received for EVERY ray as a 32-bit row hash
+(``zall_hash``, ``goldlib.row_hash`` of the float32 bits of the [S+NI]
+sorted row, VR:183: 2.5 MB per frame instead of 491 MB of depths) and, with
+ERT, each chunk's ``low_transmittance.any()`` decision per composite call
+(VR:1108-1116). A hash collision can only make two different rows look equal,
+which the tail attribution then counts as unexplained (a test failure), never
+the other way round.
 """
 from __future__ import annotations
 
@@ -155,6 +167,71 @@ def capture(name, spec, cfg, Network, vr, meta):
           f"coarse {p0:.4f} dB", flush=True)
 
 
+def capture_zall(name, spec, cfg, Network, vr, meta):
+    """Re-render `name` with the fine composite's depths hashed per ray."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from goldlib import row_hash
+    cfg.task_arg.N_importance = 128
+    cfg.task_arg.perturb = spec["perturb"]
+    cfg.task_arg.lindisp = False
+    cfg.enable_ess = spec["ess"]
+    cfg.enable_ert = spec["ert"]
+    if "thr" in spec:
+        cfg.ert_threshold = spec["thr"]
+    net = Network()
+    net.load_state_dict(torch.load(CKPT, map_location="cpu", weights_only=True)["net"])
+    net.eval()
+    rend = vr.Renderer(net)
+    rend.use_cuda_kernels = False
+    if "grid" in spec:
+        rend.occupancy_grid = torch.from_numpy(make_occupancy_grid(*spec["grid"]).copy())
+        rend.grid_update_counter = spec["counter"]
+    comp_name = "_raw2outputs_with_ert" if rend.enable_ert else "_raw2outputs"
+    orig_c = getattr(rend, comp_name)
+    calls = {"n": 0}
+    hashes, chunk_any = [], []
+
+    def rec_c(raw, z, rays_d):
+        r = orig_c(raw, z, rays_d)
+        if rend.enable_ert:          # VR:1104-1116, the chunk-wide decision of this call
+            d = torch.cat([z[..., 1:] - z[..., :-1], torch.full_like(z[..., :1], 1e10)], -1)
+            d = d * torch.norm(rays_d[..., None, :], dim=-1)
+            a = 1. - torch.exp(-torch.relu(raw[..., 3]) * d)
+            sh = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+            chunk_any.append(bool((torch.cumprod(1.0 - sh, 1) < rend.ert_threshold).any()))
+        if calls["n"] % 2 == 1:      # fine call of the chunk (VR:190-193)
+            hashes.append(row_hash(z.detach().numpy()))
+        calls["n"] += 1
+        return r
+
+    setattr(rend, comp_name, rec_c)
+    H = W = 800
+    focal = 0.5 * W / np.tan(0.5 * float(meta["camera_angle_x"]))
+    pose = np.array(meta["frames"][spec["frame"]]["transform_matrix"], np.float32)
+    K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
+    batch = {"H": H, "W": W, "pose": torch.from_numpy(pose)[None],
+             "intrinsics": torch.from_numpy(K)[None]}
+    if "seed" in spec:
+        torch.manual_seed(spec["seed"])
+    t0 = time.time()
+    with torch.no_grad():
+        ret = rend.render(batch)
+    dt = time.time() - t0
+    old = np.load(os.path.join(OUT, f"{name}.npz"))
+    for k, v in ret.items():
+        if not k.startswith("disp"):
+            assert np.array_equal(v.numpy(), old["out_" + k]), (name, k)
+    zh = np.concatenate(hashes)
+    assert zh.shape == (H * W,), zh.shape
+    path = os.path.join(OUT, f"zh_{name}.npz")
+    np.savez_compressed(path, zall_hash=zh, chunk_any=np.array(chunk_any, bool),
+                        disp_map=ret["disp_map"].numpy().astype(np.float32),
+                        disp_map_0=ret["disp_map_0"].numpy().astype(np.float32),
+                        ckpt_sha256=ckpt_sha())
+    print(f"{path}: {os.path.getsize(path) / 1e6:.1f} MB, {dt:.0f} s", flush=True)
+
+
 def add_gt(name):
     """Add the ground-truth PNG to a frame file written before it was stored."""
     p = os.path.join(OUT, f"{name}.npz")
@@ -171,11 +248,13 @@ def main(argv):
         for n in argv[1:] or list(FRAMES):
             add_gt(n)
         return
+    zall = "--zall" in argv
+    argv = [a for a in argv if a != "--zall"]
     cfg, Network, vr = _import_reference()
     meta = json.load(open(os.path.join(REF, "data/nerf_synthetic/lego/transforms_test.json")))
     names = argv or list(FRAMES)
     for n in names:
-        capture(n, FRAMES[n], cfg, Network, vr, meta)
+        (capture_zall if zall else capture)(n, FRAMES[n], cfg, Network, vr, meta)
 
 
 if __name__ == "__main__":

@@ -123,6 +123,19 @@ def load_zall(name):
 REF_CHUNK = 2048
 
 
+def row_hash(rows):
+    """32-bit FNV-1a-style hash of each row's float32 bit patterns ([n, k] -> uint32 [n]).
+    Equal rows give equal hashes; the whole-frame fixtures store the reference's
+    fine depths this way (make_ref_frames.py --zall)."""
+    w = np.ascontiguousarray(np.asarray(rows, np.float32)).view(np.uint32).astype(np.uint64)
+    h = np.full(w.shape[0], 0xCBF29CE484222325, np.uint64)
+    p = np.uint64(0x100000001B3)
+    with np.errstate(over="ignore"):
+        for j in range(w.shape[1]):
+            h = (h ^ w[:, j]) * p
+    return ((h >> np.uint64(32)) ^ (h & np.uint64(0xFFFFFFFF))).astype(np.uint32)
+
+
 def attribute_tail(ratio, z, zref, zall_hip):
     """(4) Every ray outside GATE_RATIO x the reference's spread must be explained
     by sampling, not by the MLP or the composite: its fine depths differ from the

@@ -370,3 +370,51 @@ def test_hip_adam_matches_torch_adam(dev):
         x.grad = torch.zeros_like(x)
     oc.step()
     assert float(oc.state[oc.param_groups[0]["params"][0]]["step"]) == 7.0
+
+
+def test_hip_adam_nonfinite_gradients_as_torch(dev):
+    """A NaN / +-Inf gradient goes through HipAdam's clamp as through torch's
+    clip_grad_value_ (torch.clamp keeps NaN, maps +-Inf to +-clip) and Adam:
+    the same NaN positions in the parameters and both moments, finite entries
+    within 1e-5; clip = 0 zeroes every gradient as clip_grad_value_(0) does;
+    a parameter without a gradient next to ones with is refused (one shared
+    step count)."""
+    from nerfhip.adam import HipAdam
+    g = torch.Generator(device=dev).manual_seed(7)
+    p0 = [torch.randn((256, 63), device=dev, generator=g), torch.randn((128,), device=dev, generator=g)]
+    for clip in (40.0, 0.0):
+        pa = [x.clone().requires_grad_(True) for x in p0]
+        pb = [x.clone().requires_grad_(True) for x in p0]
+        oa = HipAdam(pa, lr=5e-3, eps=1e-8, clip=clip)
+        ob = torch.optim.Adam(pb, lr=5e-3, eps=1e-8, weight_decay=0.0, foreach=False)
+        for step in range(3):
+            for a, b in zip(pa, pb):
+                gr = torch.randn(a.shape, device=dev, generator=g) * 30.0
+                if step == 1:
+                    flat = gr.view(-1)
+                    flat[::17] = float("nan")
+                    flat[5::31] = float("inf")
+                    flat[7::29] = -float("inf")
+                a.grad, b.grad = gr.clone(), gr.clone()
+            torch.nn.utils.clip_grad_value_(pb, clip)
+            oa.step()
+            ob.step()
+            for a, b in zip(pa, pb):
+                assert torch.equal(a.grad.isnan(), b.grad.isnan()), (clip, step)
+                fin = ~b.grad.isnan()
+                assert torch.equal(a.grad[fin], b.grad[fin]), (clip, step)
+                for x, y in ((a, b), (oa.state[a]["exp_avg"], ob.state[b]["exp_avg"]),
+                             (oa.state[a]["exp_avg_sq"], ob.state[b]["exp_avg_sq"])):
+                    assert torch.equal(x.isnan(), y.isnan()), (clip, step)
+                    m = ~y.isnan()
+                    if m.any():
+                        assert (x[m] - y[m]).abs().max() <= 1e-5 * y[m].abs().max().clamp_min(1e-30)
+            if step == 1 and clip == 40.0:
+                assert any(bool(a.isnan().any()) for a in pa)       # the blow-up is visible
+    pa = [x.clone().requires_grad_(True) for x in p0]
+    oa = HipAdam(pa, clip=40.0)
+    pa[0].grad = torch.zeros_like(pa[0])
+    with pytest.raises(ValueError):
+        oa.step()
+    with pytest.raises(ValueError):
+        HipAdam(pa, clip=-1.0)

@@ -22,7 +22,14 @@ from collections import defaultdict
 SHORT = {"mlp_fused_kernel": "mlp_fused", "mlp_x3_kernel": "mlp_x3", "composite_kernel": "composite",
          "composite_ert_kernel": "composite_ert", "sample_fine_kernel": "sample_fine",
          "rays_kernel": "rays", "coarse_kernel": "coarse", "ess_kernel": "ess",
-         "grid_update_kernel": "grid_update"}
+         "grid_update_kernel": "grid_update",
+         # C3 (the training step)
+         "mlp_x3_train_kernel": "mlp_x3_train", "mlp_x3_bwd_kernel": "mlp_x3_bwd",
+         "x3_wgrad_batch_kernel": "x3_wgrad_batch", "sum_partials_kernel": "sum_partials",
+         "adam_kernel": "adam", "composite_train_fwd_kernel": "composite_train_fwd",
+         "composite_train_bwd_kernel": "composite_train_bwd",
+         "sample_pdf_bwd_kernel": "sample_pdf_bwd", "x3_pack": "x3_pack",
+         "freq_encode_fm_backward_sum": "freq_encode_bwd_sum"}
 
 
 def short(name):
@@ -64,6 +71,11 @@ def summarise(per, meta):
                   "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_VALU_MFMA_F32"):
             if c in mean:
                 e[c] = mean[c]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in e and e.get("GRBM_GUI_ACTIVE"):
+            # MFMA-busy share of the kernel's cycles: the counter sums over the
+            # 1024 SIMDs, GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md)
+            e["mfma_busy_frac"] = (e["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0
+                                   / (e["GRBM_GUI_ACTIVE"] / 8.0))
         out[k] = e
     return out
 
