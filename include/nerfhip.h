@@ -328,12 +328,16 @@ int nerf_composite(const float* raw, const float* z, int64_t z_stride,
 
 /* VR:1089-1133: compositing with early ray termination, including the
  * chunk-wide argmax behaviour: rays are grouped in chunks of `chunk` rays
- * (2048 in the reference, VR:147) counted from ray 0 of this call. */
+ * (2048 in the reference, VR:147) counted from ray 0 of this call.
+ * workspace: device memory of nerf_composite_ert_workspace(n, chunk) bytes
+ * (16-B aligned; the per-ray cut maps and the per-chunk decisions of the
+ * two-pass implementation), owned by the caller, one call at a time. */
+size_t nerf_composite_ert_workspace(int64_t n, int chunk);
 int nerf_composite_ert(const float* raw, const float* z, int64_t z_stride,
                        const float* rays_d, int64_t n, int S, int white_bkgd,
                        float threshold, int chunk,
                        float* rgb, float* disp, float* acc, float* depth, float* weights,
-                       nerf_stream_t stream);
+                       void* workspace, nerf_stream_t stream);
 
 /* VR:239-268 + VR:181-183: inverse-CDF fine sampling from the coarse weights
  * and merge: z_all[n][S+n_imp] = sort(concat(z, samples)).

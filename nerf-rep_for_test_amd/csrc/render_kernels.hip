@@ -197,12 +197,25 @@ __global__ __launch_bounds__(64 * COMP_WAVES) void composite_kernel(
 // it; the map sums are per-lane then a 16-lane butterfly. No LDS.
 constexpr int COMP16_RPB = 16;   // rays per 256-thread block
 
-template <int C>
+// ERT (VR:1089-1133) in the same layout, pass 1 of 2: T is the exclusive
+// product of (1 - alpha) WITHOUT the +1e-10 (VR:1109-1111); every ray writes
+// its uncut maps to the outputs (and its weights), its cut maps -- weights
+// zeroed from `first`, the first sample with T < thr, or from 0 when no sample
+// crosses it (the argmax of an all-False row, VR:1115-1123) -- and `first` to
+// the workspace, and marks its 2048-ray chunk when it crosses the threshold.
+// Pass 2 (ert_fixup_kernel) applies the cut maps in the marked chunks.
+struct ErtCut {
+  Maps m;
+  int first;
+};
+
+template <int C, bool ERT = false>
 __global__ __launch_bounds__(256) void composite16_kernel(
     const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
     const float* __restrict__ rays_d, int64_t n, int S, int white, float* __restrict__ rgb,
     float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ depth,
-    float* __restrict__ wout) {
+    float* __restrict__ wout, float thr = 0.0f, int chunk = 1, ErtCut* __restrict__ cuts = nullptr,
+    int* __restrict__ flags = nullptr) {
   const int lane = threadIdx.x & 63, t = lane & 15;
   const int64_t ray0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
   if (ray0 >= n) return;   // wave-uniform
@@ -228,7 +241,8 @@ __global__ __launch_bounds__(256) void composite16_kernel(
     const int s = t + 16 * k;
     const float dist = ((s < S - 1) ? (zn[k] - zs[k]) : 1e10f) * nd;   // VR:290-292
     a[k] = s < S ? 1.0f - expf((-fmaxf(v[k].w, 0.0f)) * dist) : 0.0f;   // VR:288
-    p[k] = s < S ? (double)((1.0f - a[k]) + 1e-10f) : 1.0;
+    if constexpr (ERT) p[k] = s < S ? (double)(1.0f - a[k]) : 1.0;
+    else p[k] = s < S ? (double)((1.0f - a[k]) + 1e-10f) : 1.0;
   }
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) {
@@ -247,26 +261,91 @@ __global__ __launch_bounds__(256) void composite16_kernel(
   }
   Maps m{0, 0, 0, 0, 0};
   double carry = 1.0;
+  if constexpr (!ERT) {
 #pragma unroll
-  for (int k = 0; k < C; ++k) {
-    const int s = t + 16 * k;
-    const float T = (float)(carry * (t == 0 ? 1.0 : ex[k]));
-    carry = carry * tot[k];
-    const float w = a[k] * T;
-    if (s < S) {
-      if (wout && live) wout[rr * S + s] = w;
-      maps_add_fast(m, w, v[k], zs[k]);
+    for (int k = 0; k < C; ++k) {
+      const int s = t + 16 * k;
+      const float T = (float)(carry * (t == 0 ? 1.0 : ex[k]));
+      carry = carry * tot[k];
+      const float w = a[k] * T;
+      if (s < S) {
+        if (wout && live) wout[rr * S + s] = w;
+        maps_add_fast(m, w, v[k], zs[k]);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      m.r += __shfl_xor(m.r, o, 16);
+      m.g += __shfl_xor(m.g, o, 16);
+      m.b += __shfl_xor(m.b, o, 16);
+      m.d += __shfl_xor(m.d, o, 16);
+      m.a += __shfl_xor(m.a, o, 16);
+    }
+    if (t == 0 && live) maps_store(m, ray, white, rgb, disp, acc, depth);
+  } else {
+    float w[C];
+    int first = 1 << 30;   // this lane's first sample with T < thr
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int s = t + 16 * k;
+      const float T = (float)(carry * (t == 0 ? 1.0 : ex[k]));
+      carry = carry * tot[k];
+      w[k] = a[k] * T;
+      if (s < S && T < thr && first > s) first = s;
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o, 16));
+    const bool low = first < S;
+    const int f0 = low ? first : 0;   // argmax of an all-False row: 0 (quirk 1)
+    Maps c{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int s = t + 16 * k;
+      if (s < S) {
+        if (wout && live) wout[rr * S + s] = w[k];
+        maps_add(m, w[k], v[k], zs[k]);
+        maps_add(c, s < f0 ? w[k] : w[k] * 0.0f, v[k], zs[k]);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      m.r += __shfl_xor(m.r, o, 16);
+      m.g += __shfl_xor(m.g, o, 16);
+      m.b += __shfl_xor(m.b, o, 16);
+      m.d += __shfl_xor(m.d, o, 16);
+      m.a += __shfl_xor(m.a, o, 16);
+      c.r += __shfl_xor(c.r, o, 16);
+      c.g += __shfl_xor(c.g, o, 16);
+      c.b += __shfl_xor(c.b, o, 16);
+      c.d += __shfl_xor(c.d, o, 16);
+      c.a += __shfl_xor(c.a, o, 16);
+    }
+    if (t == 0 && live) {
+      maps_store(m, ray, white, rgb, disp, acc, depth);
+      cuts[ray] = ErtCut{c, f0};
+      if (low) flags[ray / chunk] = 1;   // benign race: every writer stores 1
     }
   }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    m.r += __shfl_xor(m.r, o, 16);
-    m.g += __shfl_xor(m.g, o, 16);
-    m.b += __shfl_xor(m.b, o, 16);
-    m.d += __shfl_xor(m.d, o, 16);
-    m.a += __shfl_xor(m.a, o, 16);
-  }
-  if (t == 0 && live) maps_store(m, ray, white, rgb, disp, acc, depth);
+}
+
+// ERT pass 2: in every chunk where some ray crossed the threshold, each ray
+// takes its cut maps and its weights from `first` on become w * 0 (VR:1115-1123).
+// 16 lanes per ray.
+__global__ __launch_bounds__(256) void ert_fixup_kernel(const ErtCut* __restrict__ cuts,
+                                                        const int* __restrict__ flags, int64_t n,
+                                                        int S, int chunk, int white,
+                                                        float* __restrict__ rgb,
+                                                        float* __restrict__ disp,
+                                                        float* __restrict__ acc,
+                                                        float* __restrict__ depth,
+                                                        float* __restrict__ wout) {
+  const int64_t ray = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int t = threadIdx.x & 15;
+  if (ray >= n || !flags[ray / chunk]) return;
+  const ErtCut c = cuts[ray];
+  if (t == 0) maps_store(c.m, ray, white, rgb, disp, acc, depth);
+  if (wout)
+    for (int s = c.first + t; s < S; s += 16) wout[ray * S + s] = wout[ray * S + s] * 0.0f;
 }
 
 // ERT (VR:1089-1133): if any ray of the 2048-ray chunk has T < thr, every ray's
@@ -909,19 +988,51 @@ int nerf_composite(const float* raw, const float* z, int64_t z_stride, const flo
   return check_launch("composite_kernel");
 }
 
+size_t nerf_composite_ert_workspace(int64_t n, int chunk) {
+  if (n <= 0 || chunk <= 0) return 16;
+  const size_t flags = ((size_t)cdiv(n, chunk) * sizeof(int) + 15) / 16 * 16;
+  return flags + (size_t)n * sizeof(ErtCut);
+}
+
 int nerf_composite_ert(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
                        int64_t n, int S, int white_bkgd, float threshold, int chunk, float* rgb,
-                       float* disp, float* acc, float* depth, float* weights,
+                       float* disp, float* acc, float* depth, float* weights, void* workspace,
                        nerf_stream_t stream) {
   NERF_REQUIRE(raw && z && rays_d && rgb && disp && acc && depth,
                "nerf_composite_ert: null pointer");
   NERF_REQUIRE(n >= 0 && S >= 2 && S < 1024 && chunk > 0 && chunk <= ERT_MAX_CHUNK,
                "nerf_composite_ert: need 2 <= S < 1024 and 0 < chunk <= 2048");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(composite_ert_kernel, dim3((unsigned)cdiv(n, chunk)), dim3(64 * ERT_WAVES), 0,
-                     as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S,
-                     white_bkgd, threshold, chunk, rgb, disp, acc, depth, weights);
-  return check_launch("composite_ert_kernel");
+  if (S > 256) {   // one block per chunk, the cut maps in LDS
+    hipLaunchKernelGGL(composite_ert_kernel, dim3((unsigned)cdiv(n, chunk)), dim3(64 * ERT_WAVES),
+                       0, as_stream(stream), (const float4*)raw, z, z_stride, rays_d, n, S,
+                       white_bkgd, threshold, chunk, rgb, disp, acc, depth, weights);
+    return check_launch("composite_ert_kernel");
+  }
+  NERF_REQUIRE(workspace && ((uintptr_t)workspace & 15) == 0,
+               "nerf_composite_ert: workspace (nerf_composite_ert_workspace bytes, 16-B aligned)");
+  const int64_t nch = cdiv(n, chunk);
+  int* flags = (int*)workspace;
+  ErtCut* cuts = (ErtCut*)((char*)workspace + ((size_t)nch * sizeof(int) + 15) / 16 * 16);
+  hipError_t e = hipMemsetAsync(flags, 0, (size_t)nch * sizeof(int), as_stream(stream));
+  if (e != hipSuccess) return fail((int)e, "nerf_composite_ert: flag reset failed");
+  const int c = (S + 15) / 16;
+  const dim3 grid((unsigned)cdiv(n, COMP16_RPB)), block(256);
+#define NERF_COMP16E(CC)                                                                       \
+  hipLaunchKernelGGL((composite16_kernel<CC, true>), grid, block, 0, as_stream(stream),        \
+                     (const float4*)raw, z, z_stride, rays_d, n, S, white_bkgd, rgb, disp, acc, \
+                     depth, weights, threshold, chunk, cuts, flags)
+  if (c <= 4) NERF_COMP16E(4);
+  else if (c <= 8) NERF_COMP16E(8);
+  else if (c <= 12) NERF_COMP16E(12);
+  else NERF_COMP16E(16);
+#undef NERF_COMP16E
+  const int rc = check_launch("composite16_kernel<ERT>");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ert_fixup_kernel, dim3((unsigned)cdiv(n * 16, 256)), dim3(256), 0,
+                     as_stream(stream), (const ErtCut*)cuts, (const int*)flags, n, S, chunk,
+                     white_bkgd, rgb, disp, acc, depth, weights);
+  return check_launch("ert_fixup_kernel");
 }
 
 int nerf_sample_fine(const float* z, int64_t z_stride, const float* weights, const float* u,

@@ -51,7 +51,9 @@ SIGNATURES = {
     "nerf_raw_absmax": (_I, [_P, _I64, _P, _S]),
     "nerf_freq_encode_fm_backward_sum": (_I, [_P, _P, _I64, _P, _P, _I64, _I64, _I, _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
-    "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _S]),
+    "nerf_composite_ert_workspace": (_SZ, [_I64, _I]),
+    "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _P,
+                                _S]),
     "nerf_sample_fine": (_I, [_P, _I64, _P, _P, _I64, _I64, _I, _I, _P, _S]),
     "nerf_sample_coarse_ess": (_I, [_P, _P, _P, _I, _P, _P, _I64, _I, _I, _F, _P, _S]),
     "nerf_grid_update": (_I, [_P, _P, _I64, _P, _P, _I64, _I, _P, _I, _S]),

@@ -207,8 +207,13 @@ class NerfPipeline:
         args = (ptr(raw), ptr(z), z_stride, ptr(rays_d), n, S, int(self.white_bkgd))
         tail = (ptr(rgb[off:]), ptr(disp[off:]), ptr(acc[off:]), ptr(depth[off:]), ptr(w),
                 _lib.stream_of(self.device))
-        if self.enable_ert:
-            call("nerf_composite_ert", *args, self.ert_threshold, REF_CHUNK, *tail)
+        if self.enable_ert:   # + the two-pass kernel's workspace (cut maps, chunk flags)
+            nb = int(_lib.lib().nerf_composite_ert_workspace(n, REF_CHUNK))
+            ws = torch.empty((nb,), device=self.device, dtype=torch.uint8)
+            nb = n * S * 16 + (n * S if z_stride else S) * 4 + n * 36 + (n * S * 4 if w is not None else 0)
+            self._timed("composite_ert", nb, lambda: call(
+                "nerf_composite_ert", *args, self.ert_threshold, REF_CHUNK, *tail[:-1], ptr(ws),
+                tail[-1]))
         else:   # raw 16 B/sample, z, rays_d 12 B/ray, maps 24 B/ray, weights 4 B/sample
             nb = n * S * 16 + (n * S if z_stride else S) * 4 + n * 36 + (n * S * 4 if w is not None else 0)
             self._timed("composite", nb, lambda: call("nerf_composite", *args, *tail))

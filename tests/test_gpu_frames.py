@@ -1,27 +1,37 @@
 """Whole 800x800 lego frames against the reference's OWN render (north_star:
-"PSNR within 0.01 dB on lego").
+"PSNR within 0.01 dB on lego"), ray by ray.
 
 tests/golden/r*_*.npz were rendered in the survey container by importing the
 reference's ``Renderer`` (``volume_renderer.py:109-216``, ESS/ERT
 ``:1009-1157``) with the trained checkpoint ``checkpoints/lego/latest.pth``
-(tests/golden/make_ref_frames.py), and carry the test view's ground-truth PNG.
-Here the same frames are rendered by the HIP path on cuda:0 and held to:
+(tests/golden/make_ref_frames.py), and carry the test view's ground-truth PNG;
+tests/golden/zh_r*_*.npz (``make_ref_frames.py --zall``) add the reference's
+disp maps (VR:333, NaN where acc = 0) and a hash of the fine depths of EVERY
+ray (the [192] sorted row the fine composite received, VR:183). Here the same
+frames are rendered by the HIP path on cuda:0, in both MLP precisions, and
+held to:
 
 * |PSNR_hip - PSNR_ref| <= 0.01 dB against the ground truth, PSNR as the
   reference's evaluator computes it (evaluators/nerf.py:465-473);
-* the coarse maps within 1e-5 (rgb/acc abs, depth relative) on every pixel;
-* the fine rgb within 1e-5 on >= 99 % of the pixels (the rest is the
-  ill-conditioned fine sampling: tests/goldlib.py attribute_tail, held ray by
-  ray on the crop fixtures), and PSNR(HIP vs reference) >= 60 dB;
+* the coarse maps within 1e-5 (rgb/acc abs, depth relative) and the coarse
+  disp within 1e-4 relative, NaN-aware, on every pixel;
+* every fine pixel within tolerance (rgb/acc 1e-5 abs, depth 1e-5 relative,
+  disp 1e-4 relative with the NaN pattern equal -- the quirk-1 rays of an ERT
+  chunk, VR:1115-1123, and acc = 0 rays) OR attributed: its fine depths
+  differ from the reference's (a searchsorted / denom-clamp flip of the
+  ill-conditioned fine sampling, VR:239-268; tests/goldlib.py attribute_tail)
+  or, with ERT, its 2048-ray chunk holds such a ray. tail_unexplained == 0;
+* >= 99.9 % of the pixels within tolerance on fine rgb, acc and depth, and
+  PSNR(HIP vs reference) >= 60 dB;
 * C4 (ESS + ERT): the final occupancy grid bit for bit and the call counter
   after the reference's in-frame grid self-updates (VR:1147-1155).
 
-r0 runs through NerfPipeline (the bench path) in both MLP precisions; r1
-through the drop-in plugin ``Renderer(net).render(batch)`` with the
-reference's perturb draws replayed from torch's CPU generator (seeded as the
-capture was, one [m, 64] draw per 2048-ray chunk); r2 is C4 on the bench's
-compacted-ERT path. With NERF_FRAME_REPORT=<dir> each case writes its numbers
-to <dir>/frame_parity_<name>_<prec>.json.
+r0 runs through NerfPipeline (the bench path); r1 through the drop-in plugin
+``Renderer(net).render(batch)`` with the reference's perturb draws replayed
+from torch's CPU generator (seeded as the capture was, one [m, 64] draw per
+2048-ray chunk); r2 is C4 (f16x3: the bench's compacted-ERT path; fp32: full
+evaluation). With NERF_FRAME_REPORT=<dir> each case writes its numbers to
+<dir>/frame_parity_<name>_<prec>.json.
 """
 import json
 import os
@@ -29,7 +39,7 @@ import os
 import numpy as np
 import pytest
 
-from goldlib import GOLDEN, max_err, rel_err
+from goldlib import GOLDEN, REF_CHUNK, max_err, rel_err, row_hash
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -38,6 +48,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CKPT_DIR = os.path.join(REPO, "checkpoints", "lego")
 TOL = 1e-5
 DPSNR = 0.01
+FRAC = 0.999
 
 
 @pytest.fixture(scope="module")
@@ -61,18 +72,64 @@ def _psnr(pred, gt):
     return psnr(np.asarray(pred, np.float32), gt)
 
 
-def _check(name, prec, z, got, extra=None):
+def _zh(name):
+    p = os.path.join(GOLDEN, "zh_" + name + ".npz")
+    assert os.path.exists(p), f"{p} missing: python tests/golden/make_ref_frames.py --zall"
+    return dict(np.load(p))
+
+
+def _disp(acc, depth):
+    """VR:333 in float32: 1 / max(1e-10, depth / acc) (torch.max keeps NaN)."""
+    acc = np.asarray(acc, np.float32)
+    depth = np.asarray(depth, np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = depth / acc
+        return np.float32(1.0) / np.where(np.isnan(q), q, np.maximum(np.float32(1e-10), q))
+
+
+def _pix_err(got, ref, kind):
+    """Per-pixel (error, tolerance); a NaN-pattern difference is an infinite error."""
+    a = np.asarray(got, np.float64).reshape(ref.shape[0], -1)
+    b = np.asarray(ref, np.float64).reshape(ref.shape[0], -1)
+    e = np.nan_to_num(np.abs(a - b), nan=0.0).max(-1)
+    e[(np.isnan(a) != np.isnan(b)).any(-1)] = np.inf
+    bb = np.nan_to_num(np.abs(b), nan=0.0).max(-1)
+    tol = {"abs": np.full(bb.shape, TOL), "depth": TOL * np.maximum(1.0, bb),
+           "disp": 1e-4 * np.maximum(1e-3, bb)}[kind]
+    return e, tol
+
+
+def _check(name, prec, z, got, zall_hip, extra=None):
     H, W = int(z["H"]), int(z["W"])
     n = H * W
+    zh = _zh(name)
     gt = _gt(z)
     p_ref = _psnr(z["out_rgb_map"], gt)
     assert abs(p_ref - float(z["psnr_ref"])) < 1e-6, "GT decode differs from the capture's"
+    # the stored disp maps are VR:333 of the stored depth / acc (a check of the fixture)
+    assert np.array_equal(_disp(z["out_acc_map"], z["out_depth_map"]).reshape(-1),
+                          zh["disp_map"].reshape(-1), equal_nan=True)
     p_hip = _psnr(got["rgb_map"].reshape(H, W, 3), gt)
     p0_hip = _psnr(got["rgb_map_0"].reshape(H, W, 3), gt)
-    e_rgb = np.abs(got["rgb_map"].reshape(n, 3).astype(np.float64)
-                   - z["out_rgb_map"].reshape(n, 3)).max(-1)
     diff = got["rgb_map"].reshape(n, 3).astype(np.float64) - z["out_rgb_map"].reshape(n, 3)
     mse = float(np.mean(diff ** 2))
+    fine = {"rgb": _pix_err(got["rgb_map"], z["out_rgb_map"].reshape(n, 3), "abs"),
+            "acc": _pix_err(got["acc_map"], z["out_acc_map"].reshape(n), "abs"),
+            "depth": _pix_err(got["depth_map"], z["out_depth_map"].reshape(n), "depth"),
+            "disp": _pix_err(got["disp_map"], zh["disp_map"].reshape(n), "disp")}
+    tail = np.zeros(n, bool)
+    for e, tol in fine.values():
+        tail |= e > tol
+    # ray-by-ray attribution of the tail (goldlib.attribute_tail on hashed depths)
+    ddiff = row_hash(zall_hip) != zh["zall_hash"]
+    expl = ddiff.copy()
+    if bool(z["ert"]):
+        ch = np.arange(n) // REF_CHUNK
+        cd = np.zeros(ch.max() + 1, bool)
+        np.logical_or.at(cd, ch, ddiff)
+        expl |= cd[ch]
+    unexpl = tail & ~expl
+    nan_ref = np.isnan(zh["disp_map"].reshape(n))
     rep = {"frame": name, "precision": prec, "pixels": n,
            "psnr_ref_vs_gt": p_ref, "psnr_hip_vs_gt": p_hip, "dpsnr": p_hip - p_ref,
            "psnr0_ref_vs_gt": float(z["psnr_ref_0"]), "psnr0_hip_vs_gt": p0_hip,
@@ -82,12 +139,23 @@ def _check(name, prec, z, got, extra=None):
                                          z["out_acc_map_0"].reshape(n)),
            "coarse_depth_max_rel": rel_err(got["depth_map_0"].reshape(n),
                                            z["out_depth_map_0"].reshape(n)),
-           "fine_rgb_max_abs": float(e_rgb.max()),
-           "fine_rgb_frac_within_1e-5": float(np.mean(e_rgb <= TOL)),
-           "fine_acc_max_abs": max_err(got["acc_map"].reshape(n), z["out_acc_map"].reshape(n)),
-           "fine_depth_frac_within_1e-5_rel": float(np.mean(
-               np.abs(got["depth_map"].reshape(n).astype(np.float64) - z["out_depth_map"].reshape(n))
-               <= TOL * np.maximum(1.0, np.abs(z["out_depth_map"].reshape(n))))),
+           "coarse_disp_max_rel": rel_err(got["disp_map_0"].reshape(n),
+                                          zh["disp_map_0"].reshape(n), floor=1e-3),
+           "fine_rgb_max_abs": float(fine["rgb"][0].max()),
+           **{f"fine_{k}_frac_within_tol": float(np.mean(e <= tol)) for k, (e, tol) in fine.items()},
+           "disp_nan_ref": int(nan_ref.sum()),
+           "disp_nan_hip": int(np.isnan(got["disp_map"].reshape(n)).sum()),
+           "rays_with_other_fine_depths": int(ddiff.sum()),
+           "tail_pixels": int(tail.sum()), "tail_unexplained": int(unexpl.sum()),
+           "tail_unexplained_by_map": {k: int((unexpl & (e > tol)).sum())
+                                       for k, (e, tol) in fine.items()},
+           "tail_unexplained_detail": [
+               {"pixel": int(i), "acc_ref": float(z["out_acc_map"].reshape(n)[i]),
+                "acc_hip": float(got["acc_map"].reshape(n)[i]),
+                "depth_ref": float(z["out_depth_map"].reshape(n)[i]),
+                "depth_hip": float(got["depth_map"].reshape(n)[i]),
+                **{f"{k}_err": float(e[i]) for k, (e, _) in fine.items()}}
+               for i in np.flatnonzero(unexpl)[:20]],
            "psnr_hip_vs_ref": float("inf") if mse == 0 else -10 * np.log10(mse),
            "reference_cpu_seconds": float(z["cpu_seconds"])}
     if extra:
@@ -102,7 +170,10 @@ def _check(name, prec, z, got, extra=None):
     assert rep["coarse_rgb_max_abs"] <= TOL, rep
     assert rep["coarse_acc_max_abs"] <= TOL, rep
     assert rep["coarse_depth_max_rel"] <= TOL, rep
-    assert rep["fine_rgb_frac_within_1e-5"] >= 0.99, rep
+    assert rep["coarse_disp_max_rel"] <= 1e-4, rep
+    for k in ("rgb", "acc", "depth"):
+        assert rep[f"fine_{k}_frac_within_tol"] >= FRAC, rep
+    assert rep["tail_unexplained"] == 0, rep
     assert rep["psnr_hip_vs_ref"] >= 60.0, rep
     return rep
 
@@ -113,11 +184,20 @@ def test_c2_frame0_vs_reference(dev, prec):
     z = _frame("r0_c2_frame0")
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128, mlp_precision=prec)
     pipe.load_checkpoint(CKPT_DIR)
+    pipe.capture_zall = []
     res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"])
-    _check("r0_c2_frame0", prec, z, {k: v.cpu().numpy() for k, v in res.items()})
+    _check("r0_c2_frame0", prec, z, {k: v.cpu().numpy() for k, v in res.items()},
+           _zall(pipe))
 
 
-def test_c2_perturbed_frame_through_plugin(dev):
+def _zall(pipe):
+    zall = torch.cat(pipe.capture_zall).cpu().numpy()
+    pipe.capture_zall = None
+    return zall
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "fp32"])
+def test_c2_perturbed_frame_through_plugin(dev, prec):
     """The drop-in Renderer, perturb 1 at eval (lego.yaml:22): the plugin's
     per-chunk draws are served from torch's CPU generator seeded like the
     capture, i.e. the very numbers the reference consumed."""
@@ -129,6 +209,7 @@ def test_c2_perturbed_frame_through_plugin(dev):
     cfg.task_arg.perturb = 1
     cfg.enable_ess = False
     cfg.enable_ert = False
+    cfg.mlp_precision = prec
     net = Network().to(dev)
     sd = torch.load(os.path.join(CKPT_DIR, "latest.pth"), map_location="cpu",
                     weights_only=True)["net"]
@@ -144,6 +225,7 @@ def test_c2_perturbed_frame_through_plugin(dev):
         return orig(size, generator=gen).to(device)
     batch = {"H": int(z["H"]), "W": int(z["W"]), "pose": torch.from_numpy(z["pose"])[None],
              "intrinsics": torch.from_numpy(z["K"])[None]}
+    rend.pipeline.capture_zall = []
     torch.rand = rand
     try:
         with torch.no_grad():
@@ -153,10 +235,12 @@ def test_c2_perturbed_frame_through_plugin(dev):
         reset()
     n = int(z["H"]) * int(z["W"])
     assert sizes == [(min(2048, n - c), 64) for c in range(0, n, 2048)]
-    _check("r1_c2_frame8_pert", "f16x3", z, {k: v.cpu().numpy() for k, v in out.items()})
+    _check("r1_c2_frame8_pert", prec, z, {k: v.cpu().numpy() for k, v in out.items()},
+           _zall(rend.pipeline))
 
 
-def test_c4_frame16_vs_reference(dev):
+@pytest.mark.parametrize("prec", ["f16x3", "fp32"])
+def test_c4_frame16_vs_reference(dev, prec):
     """ESS + ERT at full frame: 313 chunks, the reference's grid self-updates at
     calls 0 and 500 inside the frame, ERT termination and its chunk-wide
     argmax rule on real lego content; compacted ERT MLP (the bench path)."""
@@ -164,18 +248,20 @@ def test_c4_frame16_vs_reference(dev):
     from nerfhip.synthetic import make_occupancy_grid
     z = _frame("r2_c4_frame16")
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
-                        ert_threshold=float(z["thr"]), mlp_precision="f16x3")
+                        ert_threshold=float(z["thr"]), mlp_precision=prec)
     pipe.load_checkpoint(CKPT_DIR)
     gs = z["grid_spec"]
     pipe.set_grid(make_occupancy_grid(int(gs[0]), int(gs[1]), float(gs[2]), float(gs[3])))
     pipe.grid_update_counter = int(z["counter0"])
+    pipe.capture_zall = []
     res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     ev, full = pipe.evaluated_samples()
     got = {k: v.cpu().numpy() for k, v in res.items()}
     grid_ok = np.array_equal(np.packbits(pipe.grid.cpu().numpy().astype(bool)),
                              z["grid_final_bits"])
-    rep = _check("r2_c4_frame16", "f16x3", z, got,
+    rep = _check("r2_c4_frame16", prec, z, got, _zall(pipe),
                  {"grid_final_equal": bool(grid_ok), "counter": pipe.grid_update_counter,
                   "evaluated_sample_frac": ev / max(full, 1)})
+    assert rep["disp_nan_ref"] > 0, rep          # the frame exercises quirk 1 / acc = 0
     assert pipe.grid_update_counter == int(z["grid_counter_final"]), rep
     assert grid_ok, rep
