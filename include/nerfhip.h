@@ -251,6 +251,14 @@ typedef struct NerfX3TrainOut {
 int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_head, const float* pts,
                               const float* dirs, const float* zero, int64_t P,
                               const NerfX3TrainOut* out, float* raw, nerf_stream_t stream);
+/* The same over the samples of n rays (VR:165): sample p = ray * S + step at
+ * rays_o[ray] + rays_d[ray] * z[ray * z_stride + step], view direction
+ * rays_d[ray]; P = n * S (the point tensor and the per-sample directions are
+ * never materialised). */
+int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float* w_head,
+                                   const float* rays_o, const float* rays_d, const float* z,
+                                   int64_t z_stride, int64_t n, int S, const NerfX3TrainOut* out,
+                                   float* raw, nerf_stream_t stream);
 
 /* nerf_mlp_train_backward_x3: the backward through the training MLP (the
  *   dgrad chain) in ONE launch, over the transposed-weight stream of
@@ -307,6 +315,11 @@ int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
                                      const float* enc, const float* x, int64_t ldx, int64_t P,
                                      int n_freq, float* dx, nerf_stream_t stream);
+/* ... taken on to the sample depths of nerf_mlp_train_forward_x3_rays: dz[p] =
+ * sum_c dx[p][c] * rays_d[p / S][c] (enc required). */
+int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int64_t ldd,
+                                    const float* enc, const float* rays_d, int S, int64_t P,
+                                    int n_freq, float* dz, nerf_stream_t stream);
 /* nerf_x3_pack: packs n weight matrices for the x3 training kernels in one
  * launch set. descs (device) = n records {const float* src; int64_t ldr, ldc;
  * const int* rowmap; const int* colmap; int M, K; void* out; int* sw;

@@ -884,6 +884,38 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
   }
 }
 
+// The same gradient taken on to the depths of the samples p = ray * S + step
+// at o + d * z (VR:165; rays constant): dz[p] = sum_c dx_c * d_c, as torch's
+// autograd of rays_o + rays_d * z sums it (mul, then the 3-term reduction).
+__global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
+    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P, int L,
+    float* __restrict__ dz) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  auto de = [&](int row) {
+    float v = d_enc[row * ldd + p];
+    if (d_enc2) v = v + d_enc2[row * ldd + p];
+    return v;
+  };
+  const int64_t ray = p / S;
+  float acc = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float g = de(c);
+    for (int f = 0; f < L; ++f) {
+      const float k = (float)(1 << f);
+      const float sn = enc[(3 + 6 * f + c) * ldd + p];
+      const float cs = enc[(6 + 6 * f + c) * ldd + p];
+      const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
+      g = g + ds * k;
+    }
+    const float t = g * rays_d[ray * 3 + c];
+    acc = c == 0 ? t : acc + t;
+  }
+  dz[p] = acc;
+}
+
 // max |rgb| / |sigma| of raw [P][4] (float bits: the values are >= 0)
 __global__ __launch_bounds__(256) void raw_absmax_kernel(const float4* __restrict__ raw, int64_t P,
                                                          unsigned* __restrict__ amax) {
@@ -1106,6 +1138,18 @@ int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream) {
   return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, nullptr, x, ldx, P, n_freq, dx,
                                           stream);
+}
+
+int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int64_t ldd,
+                                    const float* enc, const float* rays_d, int S, int64_t P,
+                                    int n_freq, float* dz, nerf_stream_t stream) {
+  NERF_REQUIRE(d_enc && enc && rays_d && dz, "nerf_freq_encode_fm_backward_dz: null pointer");
+  NERF_REQUIRE(P >= 0 && S >= 1 && P % S == 0 && ldd >= P && n_freq >= 0 && n_freq <= 24,
+               "nerf_freq_encode_fm_backward_dz: bad size");
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
+                     as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P, n_freq, dz);
+  return check_launch("freq_encode_fm_backward_dz_kernel");
 }
 
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,

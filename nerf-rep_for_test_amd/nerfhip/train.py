@@ -139,8 +139,15 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
     if composite_fn is None:
         def composite_fn(raw, zz, rd):
             return composite(raw, zz, rd, white_bkgd)
-    pts = rays_o[:, None, :] + rays_d[:, None, :] * z[..., None]
-    raw = query_fn(coarse, pts, rays_d)
+    # a query with a ray form (train_mlp.query_x3.rays) builds the points o + d z
+    # itself (VR:165) and returns d z directly in the backward
+    rays_q = getattr(query_fn, "rays", None)
+
+    def q(model, zz):
+        if rays_q is not None:
+            return rays_q(model, rays_o, rays_d, zz)
+        return query_fn(model, rays_o[:, None, :] + rays_d[:, None, :] * zz[..., None], rays_d)
+    raw = q(coarse, z)
     rgb0, disp0, acc0, w, depth0 = composite_fn(raw, z, rays_d)
     if on_composite is not None:
         on_composite(0, z, raw, w)
@@ -155,8 +162,7 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
             if detach_fine_samples:
                 zf = zf.detach()
             z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
-        pts2 = rays_o[:, None, :] + rays_d[:, None, :] * z2[..., None]
-        raw2 = query_fn(fine, pts2, rays_d)
+        raw2 = q(fine, z2)
         rgb, disp, acc, w2, depth = composite_fn(raw2, z2, rays_d)
         if on_composite is not None:
             on_composite(1, z2, raw2, w2)

@@ -752,16 +752,17 @@ class NerfMLPFn(torch.autograd.Function):
         return raw
 
     @staticmethod
-    def _forward_fused(ctx, pts, pts_c, dirs, params, E, H, amax, pk):
+    def _forward_fused(ctx, pts, pts_c, dirs, params, E, H, amax, pk, rays=None):
         """The forward as ONE nerf_mlp_train_forward_x3 launch (the inference
         kernel's per-tile body over the unfolded stream, writing every layer's
         output rows, ReLU bits and max |.|): what the ten layer launches of the
-        unfused forward produce, and the backward reads."""
-        dev = pts.device
-        P = pts.shape[0]
+        unfused forward produce, and the backward reads. rays = (rays_o, rays_d,
+        z) (RayMLPFn): the samples o + d z of the rays instead of pts / dirs."""
+        dev = E.device
+        P = E.shape[1]
         stream, head = ctx.streams[:2]
         V = _act(288, P, dev)      # cat(feature, views enc, 5 zero rows): all from the kernel
-        dirs_c = dirs.detach().contiguous()
+        dirs_c = dirs.detach().contiguous() if rays is None else None
         HV = _act(128, P, dev)
         bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
         bits_v = torch.empty((relu_bits_words(P, 8),), device=dev, dtype=torch.int16)
@@ -781,10 +782,19 @@ class NerfMLPFn(torch.autograd.Function):
         out.amax = amax.data_ptr()
         out.ld = H[0].stride(0)
         assert all(t.stride(0) == out.ld for t in (E, V, HV)) and H[0].stride(1) == 1
-        call("nerf_mlp_train_forward_x3", ptr(stream), ptr(head), ptr(pts_c), ptr(dirs_c),
-             ptr(zero), P, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
-        ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
-        ctx.pts_grad = pts.requires_grad
+        if rays is None:
+            call("nerf_mlp_train_forward_x3", ptr(stream), ptr(head), ptr(pts_c), ptr(dirs_c),
+                 ptr(zero), P, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
+            ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
+            ctx.pts_grad = pts.requires_grad
+        else:
+            ro, rd, z = rays
+            n, S = z.shape
+            call("nerf_mlp_train_forward_x3_rays", ptr(stream), ptr(head), ptr(ro), ptr(rd),
+                 ptr(z), S, n, S, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
+            # the rays' directions stand where the points do: d z = sum_c d pts_c d_c
+            ctx.save_for_backward(rd, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
+            ctx.pts_grad = z.requires_grad
         ctx.packs = pk
         return raw
 
@@ -817,7 +827,8 @@ class NerfMLPFn(torch.autograd.Function):
         # sums), not from separate reductions over P
         post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
-        need_enc = ctx.pts_grad and ctx.needs_input_grad[0]
+        rays_S = getattr(ctx, "rays_S", 0)   # RayMLPFn: the gradient goes to z [n, S]
+        need_enc = ctx.pts_grad and ctx.needs_input_grad[2 if rays_S else 0]
         if ctx.fused_backward:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(d_raw_c, ctx.streams[2:], bits, bits_v,
                                                            dmax, need_enc)
@@ -847,12 +858,20 @@ class NerfMLPFn(torch.autograd.Function):
                 grads[bname] = gb
         d_pts = None
         if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
-            d_pts = torch.empty((P, 3), device=dev, dtype=f32)
             assert d_enc[0].stride(0) == d_enc[1].stride(0)
             assert E.stride(0) == d_enc[0].stride(0)
-            call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]),
-                 d_enc[0].stride(0), ptr(E), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
-                 _lib.stream_of(dev))
+            if rays_S:          # pts = the rays' o + d z: straight on to d z
+                d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
+                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]),
+                     d_enc[0].stride(0), ptr(E), ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
+                     _lib.stream_of(dev))
+            else:
+                d_pts = torch.empty((P, 3), device=dev, dtype=f32)
+                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]),
+                     d_enc[0].stride(0), ptr(E), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
+                     _lib.stream_of(dev))
+        if rays_S:
+            return (None, None, d_pts, *[grads[n] for n in PARAM_NAMES])
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
 
 
@@ -935,6 +954,45 @@ NerfMLPFn._backward_layers = staticmethod(_backward_layers_impl)
 NerfMLPFn._backward_fused = staticmethod(_backward_fused_impl)
 
 
+class RayMLPFn(torch.autograd.Function):
+    """raw [n, S, 4] = NeRF(encodings of the samples rays_o + rays_d * z, VR:165,
+    with view direction rays_d) on the fused x3 kernels, without the point
+    tensor or the per-sample directions: the forward kernel builds each point
+    from its ray (nerf_mlp_train_forward_x3_rays) and the backward returns the
+    gradient w.r.t. z [n, S] (nerf_freq_encode_fm_backward_dz: sum_c d pts_c
+    d_c, the autograd of o + d z with constant rays). Inputs: rays_o [n, 3],
+    rays_d [n, 3] (no gradient), z [n, S], then the 24 parameters."""
+
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, z, *params):
+        n, S = z.shape
+        P = n * S
+        dev = z.device
+        E = _act(320, P, dev)
+        amax = torch.zeros(12, device=dev, dtype=torch.float32)
+        H = [_act(256, P, dev) if i != 4 else None for i in range(8)]
+        H[4] = E[64:320]
+        ctx.fused_backward = FUSED_BACKWARD and P > 0
+        ctx.streams = _streams_for(params, dev)
+        ctx.rays_S = S
+        pk = None if ctx.fused_backward else _packs_for(params, dev, forward=False, backward=True)
+        rays = (rays_o.detach().contiguous(), rays_d.detach().contiguous(),
+                z.detach().contiguous())
+        raw = NerfMLPFn._forward_fused(ctx, None, None, None, params, E, H, amax, pk, rays)
+        return raw.view(n, S, 4)
+
+    @staticmethod
+    def backward(ctx, d_raw):
+        return NerfMLPFn.backward(ctx, d_raw.reshape(-1, 4))
+
+
+def query_x3_rays(model, rays_o, rays_d, z):
+    """query_x3 of the samples rays_o + rays_d * z (VR:164-165, 270-284) with no
+    point tensor: raw [n, S, 4], differentiable in z and the parameters."""
+    _lib.require_gpu(z)
+    return RayMLPFn.apply(rays_o, rays_d, z, *mlp_params(model))
+
+
 def mlp_params(model):
     """The 24 parameters of a reference NeRF module in PARAM_NAMES order."""
     named = dict(model.named_parameters())
@@ -942,9 +1000,15 @@ def mlp_params(model):
 
 
 def query_x3(model, pts, dirs):
-    """Drop-in for train.query (VR:270-284): pts [n, s, 3], dirs [n, 3]."""
+    """Drop-in for train.query (VR:270-284): pts [n, s, 3], dirs [n, 3]
+    (train.render_train takes query_x3.rays, the ray form, when the fused
+    forward is on)."""
     n, s, _ = pts.shape
     _lib.require_gpu(pts)
     d = dirs[:, None, :].expand(n, s, 3).reshape(-1, 3)
     raw = NerfMLPFn.apply(pts.reshape(-1, 3), d, *mlp_params(model))
     return raw.reshape(n, s, 4)
+
+
+if FUSED_FORWARD:
+    query_x3.rays = query_x3_rays

@@ -61,10 +61,30 @@ def _elementwise_grads(name, grads, coarse=False):
         ref = tg[key + k].astype(np.float64).reshape(-1)
         got = g.detach().double().cpu().numpy().reshape(-1)
         rel = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)
-        bound = 2.0 * float(tg[dkey + k]) + floor
-        worst[k] = (rel, bound)
-        assert rel <= bound, (k, rel, bound)
+        worst[k] = (rel, float(tg[dkey + k]))
+    _report(name, "coarse" if coarse else "full", worst)
+    for k, (rel, d) in worst.items():
+        assert rel <= 2.0 * d + floor, (k, rel, 2.0 * d + floor)
     return worst
+
+
+def _report(name, kind, worst):
+    """Print (and with NERF_FRAME_REPORT=<dir> write) every tensor's measured
+    relative distance next to the reference's own self-distance."""
+    import json
+    import os
+    rows = {k: {"rel": r, "ref_self": d, "ratio": r / d if d > 0 else None}
+            for k, (r, d) in sorted(worst.items())}
+    print(json.dumps({"case": name, "loss": kind, "grads": rows}))
+    out = os.environ.get("NERF_FRAME_REPORT")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, f"grad_dist_{name}_{kind}_{len(_REPORTS)}.json"), "w") as f:
+            json.dump(rows, f, indent=1)
+    _REPORTS.append(name)
+
+
+_REPORTS = []
 
 
 def _setup(dev, mlp="x3", ops="hip"):

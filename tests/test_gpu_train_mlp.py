@@ -503,3 +503,36 @@ def test_net_packer_packs_live_parameters(dev):
     check(m, train_mlp._streams_for(mlp_params(m), dev))     # prepack's packing, not a new one
     check(m2, train_mlp._streams_for(mlp_params(m2), dev))
     assert not any(n.pending for n in nets)
+
+
+@pytest.mark.parametrize("n,S", [(1, 1), (37, 64), (300, 192)])
+def test_ray_form_equals_point_form(dev, n, S):
+    """RayMLPFn (the points o + d z built in the forward kernel, VR:165; the
+    backward straight to d z) against NerfMLPFn on the torch-built points
+    rays_o + rays_d * z with per-sample directions: raw and every parameter
+    gradient bitwise equal (the same kernels on the same float32 points), d z
+    equal to torch's autograd of o + d z through the point gradient within one
+    rounding of its 3-term sum."""
+    from nerfhip.train_mlp import NerfMLPFn, RayMLPFn, PARAM_NAMES, mlp_params
+    m = _model(dev)
+    g = torch.Generator().manual_seed(3)
+    ro = (torch.rand((n, 3), generator=g) * 2.0 - 1.0).to(dev)
+    rd = torch.nn.functional.normalize(torch.randn((n, 3), generator=g), dim=1).to(dev)
+    z0 = (2.0 + 4.0 * torch.rand((n, S), generator=g)).to(dev)
+    d_raw = torch.randn((n, S, 4), generator=torch.Generator().manual_seed(4)).to(dev)
+
+    z1 = z0.clone().requires_grad_(True)
+    pts = ro[:, None, :] + rd[:, None, :] * z1[..., None]
+    dirs = rd[:, None, :].expand(n, S, 3).reshape(-1, 3)
+    ref = NerfMLPFn.apply(pts.reshape(-1, 3), dirs, *mlp_params(m)).reshape(n, S, 4)
+    ref_g = torch.autograd.grad(ref, [z1] + mlp_params(m), d_raw)
+
+    z2 = z0.clone().requires_grad_(True)
+    out = RayMLPFn.apply(ro, rd, z2, *mlp_params(m))
+    got_g = torch.autograd.grad(out, [z2] + mlp_params(m), d_raw)
+    assert torch.equal(out.detach(), ref.detach())
+    for name, a, b in zip(PARAM_NAMES, got_g[1:], ref_g[1:]):
+        assert torch.equal(a, b), name
+    dz, dz_ref = got_g[0], ref_g[0]
+    assert dz.shape == (n, S)
+    assert float((dz - dz_ref).abs().max()) <= 1e-6 * float(dz_ref.abs().max().clamp_min(1e-30))
