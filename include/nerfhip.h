@@ -134,6 +134,14 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 /* nerf_sum_partials: out[i] = sum_{c=0}^{C-1} part[c * n + i], summed in c
  *   order (the weight-gradient split-K partials of nerf_x3_wgrad). */
 int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream);
+/* trainers/nerf.py:39-76: out[0] = mean((a - target)^2), out[1] = the same of b
+ * (0 when b is NULL), out[2] = out[0] + out[1] (a, b, target: N floats; one
+ * workgroup). Backward: g[3] = d out; da = (2/N)(a - t)(g[0] + g[2]), db =
+ * (2/N)(b - t)(g[1] + g[2]). */
+int nerf_mse_pair(const float* a, const float* b, const float* target, int64_t N, float* out,
+                  nerf_stream_t stream);
+int nerf_mse_pair_backward(const float* a, const float* b, const float* target, int64_t N,
+                           const float* g, float* da, float* db, nerf_stream_t stream);
 int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
                         const float* g_zall, int64_t n, int S, int n_imp,
                         float* d_weights, nerf_stream_t stream);

@@ -361,7 +361,76 @@ __global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
   }
 }
 
+// The training loss (trainers/nerf.py:39-76): mean squared error of the
+// coarse and the fine rgb against the target, and their sum, in ONE workgroup
+// (n * 3 elements; float32 per-thread sums, then a fixed tree over the block);
+// its backward: d a = (2 / N) * (a - t) * g for both maps in one launch
+// (torch's mse_loss_backward: norm * (input - target) * grad_output).
+constexpr int kMseThreads = 1024;
+__global__ __launch_bounds__(kMseThreads) void mse_pair_kernel(const float* __restrict__ a,
+                                                              const float* __restrict__ b,
+                                                              const float* __restrict__ t,
+                                                              int64_t N, float* __restrict__ out) {
+  __shared__ float sa[kMseThreads], sb[kMseThreads];
+  float ua = 0.0f, ub = 0.0f;
+  for (int64_t i = threadIdx.x; i < N; i += kMseThreads) {
+    const float da = a[i] - t[i];
+    ua += da * da;
+    if (b) {
+      const float db = b[i] - t[i];
+      ub += db * db;
+    }
+  }
+  sa[threadIdx.x] = ua;
+  sb[threadIdx.x] = ub;
+  __syncthreads();
+  for (int o = kMseThreads / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sa[threadIdx.x] += sa[threadIdx.x + o];
+      sb[threadIdx.x] += sb[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float lc = sa[0] / (float)N, lf = sb[0] / (float)N;
+    out[0] = lc;
+    out[1] = lf;
+    out[2] = b ? lc + lf : lc;
+  }
+}
+
+__global__ __launch_bounds__(256) void mse_pair_bwd_kernel(const float* __restrict__ a,
+                                                           const float* __restrict__ b,
+                                                           const float* __restrict__ t, int64_t N,
+                                                           const float* __restrict__ g,
+                                                           float* __restrict__ da,
+                                                           float* __restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const float norm = 2.0f / (float)N;
+  // g: d loss_c, d loss_f, d (loss_c + loss_f)
+  const float gc = g[0] + g[2], gf = g[1] + g[2];
+  da[i] = norm * (a[i] - t[i]) * gc;
+  if (b) db[i] = norm * (b[i] - t[i]) * gf;
+}
+
 extern "C" {
+
+int nerf_mse_pair(const float* a, const float* b, const float* target, int64_t N, float* out,
+                  nerf_stream_t stream) {
+  NERF_REQUIRE(a && target && out && N > 0, "nerf_mse_pair: bad arguments");
+  hipLaunchKernelGGL(mse_pair_kernel, dim3(1), dim3(kMseThreads), 0, as_stream(stream), a, b,
+                     target, N, out);
+  return check_launch("mse_pair_kernel");
+}
+
+int nerf_mse_pair_backward(const float* a, const float* b, const float* target, int64_t N,
+                           const float* g, float* da, float* db, nerf_stream_t stream) {
+  NERF_REQUIRE(a && target && g && da && (!b || db) && N > 0, "nerf_mse_pair_backward: bad arguments");
+  hipLaunchKernelGGL(mse_pair_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0,
+                     as_stream(stream), a, b, target, N, g, da, db);
+  return check_launch("mse_pair_bwd_kernel");
+}
 
 int nerf_composite_train_fwd(const float* raw, const float* z, const float* rays_d, int64_t n,
                              int S, int white, float* rgb, float* disp, float* acc, float* depth,

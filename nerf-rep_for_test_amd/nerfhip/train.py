@@ -324,6 +324,9 @@ class NerfTrainer:
                             hip_ops=self.ops == "hip")
 
     def loss(self, out, target):
+        if self.ops == "hip":   # one launch forward, one backward (train_ops.MSEPairFn)
+            from .train_ops import mse_losses_hip
+            return mse_losses_hip(out, target)
         return mse_losses(out, target)
 
     def set_lr(self, lr):

@@ -94,3 +94,42 @@ def composite_hip(raw, z, rays_d, white_bkgd=True):
 def sample_fine_hip(weights, z, u):
     _lib.require_gpu(z)
     return SampleFineFn.apply(weights, z, u)
+
+
+class MSEPairFn(torch.autograd.Function):
+    """(loss_coarse, loss_fine, loss) = (mse(a, t), mse(b, t), their sum)
+    (trainers/nerf.py:39-76) in one launch, its backward in one; b may be None
+    (no fine pass: loss_fine = 0)."""
+
+    @staticmethod
+    def forward(ctx, a, b, target):
+        a_c, t_c = a.detach().contiguous(), target.detach().contiguous()
+        b_c = b.detach().contiguous() if b is not None else None
+        out = torch.empty(3, device=a.device, dtype=torch.float32)
+        call("nerf_mse_pair", ptr(a_c), ptr(b_c), ptr(t_c), a_c.numel(), ptr(out),
+             _lib.stream_of(a.device))
+        ctx.save_for_backward(a_c, b_c, t_c)
+        ctx.has_b = b is not None
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, g0, g1, g2):
+        a, b, t = ctx.saved_tensors
+        g = torch.stack([x if x is not None else torch.zeros((), device=a.device)
+                         for x in (g0, g1, g2)]).to(torch.float32).contiguous()
+        da = torch.empty_like(a)
+        db = torch.empty_like(b) if ctx.has_b else None
+        call("nerf_mse_pair_backward", ptr(a), ptr(b), ptr(t), a.numel(), ptr(g), ptr(da),
+             ptr(db), _lib.stream_of(a.device))
+        return da, db, None
+
+
+def mse_losses_hip(out, target):
+    """trainers/nerf.py:39-76 as mse_losses, on the fused loss kernel."""
+    _lib.require_gpu(target)
+    fine = out.get("rgb_map")
+    lc, lf, loss = MSEPairFn.apply(out["rgb_map_0"], fine, target)
+    res = {"loss_coarse": lc, "loss": loss}
+    if fine is not None:
+        res["loss_fine"] = lf
+    return res
