@@ -519,10 +519,31 @@ def train_roofline(mlp, flop, step_s):
     else:
         kernel, achieved, peak, unit = ("whole step (MLP GEMMs on hipBLASLt dominate)", algo,
                                         FP32_MFMA_PEAK_TFLOPS, "TFLOP/s")
-    return {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit,
-            "frac": achieved / peak, "algorithmic_tflops": algo,
-            "frac_of_fp32_peak": algo / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-            "flop_per_step": flop}
+    out = {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": unit,
+           "frac": achieved / peak, "algorithmic_tflops": algo,
+           "frac_of_fp32_peak": algo / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+           "flop_per_step": flop}
+    c3 = c3_pmc_summary() if mlp == "x3" else None
+    if c3:
+        # measured HBM bytes per step (rocprofv3 PMC, profiles/*_c3_pmc_summary.json):
+        # the step moves every activation and its gradient through HBM once each way
+        out.update(traffic=c3["hbm_bytes_per_step"], traffic_unit="HBM bytes per step (PMC)",
+                   hbm_TBps=c3["hbm_bytes_per_step"] / step_s / 1e12,
+                   hbm_frac=c3["hbm_bytes_per_step"] / step_s / HBM_PEAK_BPS,
+                   kernels_hbm_bytes_per_step={
+                       k: round(v["hbm_bytes_per_step"]) for k, v in c3["kernels"].items()
+                       if v["hbm_bytes_per_step"] > 1e8})
+    return out
+
+
+def c3_pmc_summary():
+    """The newest committed C3 PMC summary (tools/pmc_step_summary.py), else None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_c3_pmc_summary.json"))):
+        with open(f) as fh:
+            best = json.load(fh)
+    return best
 
 
 DTYPES = {"fp32": "fp32",
@@ -562,6 +583,9 @@ def roofline(precision, timer, elapsed, world, H, W, pmc_workload=True):
             "algorithmic_tflops": algo_tflops,
             "frac_of_fp32_peak": algo_tflops / FP32_MFMA_PEAK_TFLOPS,
             "traffic": pmc_traffic(H, W, kernel) if pmc_workload else None,
+            # the share of the kernel's cycles its MFMA pipes were busy (PMC, committed
+            # summary of the same workload): the clock-independent view of `frac`
+            "mfma_busy_pmc": pmc_entry(H, W, kernel, "mfma_busy_frac") if pmc_workload else None,
             "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
             "algorithmic_bytes_per_launch": mlp_bytes / max(1, n_launch),
             "lds_staged_bytes_per_launch": staged / max(1, n_launch),
@@ -589,9 +613,10 @@ def byte_kernels(stages, steps):
     return out
 
 
-def pmc_traffic(H, W, kernel="mlp_fused_kernel"):
-    """Measured HBM bytes per MLP launch from the newest committed PMC summary
-    (tools/pmc.sh + tools/pmc_summary.py) taken on this same workload, else None."""
+def pmc_entry(H, W, kernel="mlp_fused_kernel", key="hbm_bytes_per_launch"):
+    """A measured per-launch figure of the MLP kernel from the newest committed PMC
+    summary (tools/pmc.sh + tools/pmc_summary.py) taken on this same workload,
+    else None."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_summary.json"))):
@@ -599,9 +624,18 @@ def pmc_traffic(H, W, kernel="mlp_fused_kernel"):
             doc = json.load(fh)
         wl = doc.get("workload", {})
         e = doc.get("kernels", {}).get(kernel.replace("_kernel", ""), {})
-        if wl.get("H") == H and wl.get("W") == W and "hbm_bytes_per_launch" in e:
-            best = e["hbm_bytes_per_launch"]
+        if wl.get("H") == H and wl.get("W") == W:
+            if key in e:
+                best = e[key]
+            elif key == "mfma_busy_frac" and e.get("GRBM_GUI_ACTIVE"):
+                # SQ_VALU_MFMA_BUSY_CYCLES sums over the 1024 SIMDs, GRBM_GUI_ACTIVE
+                # over the 8 XCDs (MI355X_MICROARCH.md)
+                best = e["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024.0 / (e["GRBM_GUI_ACTIVE"] / 8.0)
     return best
+
+
+def pmc_traffic(H, W, kernel="mlp_fused_kernel"):
+    return pmc_entry(H, W, kernel)
 
 
 def _strip(H, W, rows):

@@ -351,6 +351,12 @@ __device__ __forceinline__ void lds_max_u32(unsigned* p, unsigned v) {
                : "memory");
 }
 
+// cache policy of the training kernels' activation / gradient row stores
+// (buffer instruction aux bits; timing A/B through `make variant`)
+#ifndef NERF_ACT_STORE_AUX
+#define NERF_ACT_STORE_AUX 0
+#endif
+
 struct ActStore {
   __amdgpu_buffer_rsrc_t rs;   // the layer's output rows (num_records: rows * ld * 4)
   __amdgpu_buffer_rsrc_t rb;   // its ReLU-bit words (num_records 0: no bits)
@@ -370,9 +376,9 @@ struct ActStore {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, (int)vo,
-                                            (int)((32 * G + r) * ld4), 0);
+                                            (int)((32 * G + r) * ld4), NERF_ACT_STORE_AUX);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + r]), rs, (int)vo,
-                                            (int)((32 * G + 16 + r) * ld4), 0);
+                                            (int)((32 * G + 16 + r) * ld4), NERF_ACT_STORE_AUX);
     }
     if (bits) {   // bit 4t + r of the block word = (h > 0): post-ReLU h >= 0
       unsigned m = 0u;

@@ -17,7 +17,8 @@ held to:
   disp within 1e-4 relative, NaN-aware, on every pixel;
 * every fine pixel within tolerance (rgb/acc 1e-5 abs, depth 1e-5 relative,
   disp 1e-4 relative with the NaN pattern equal -- the quirk-1 rays of an ERT
-  chunk, VR:1115-1123, and acc = 0 rays) OR attributed: its fine depths
+  chunk, VR:1115-1123, and acc = 0 rays -- wherever either render's acc
+  exceeds 1e-6, SURVEY §8c's disp rule) OR attributed: its fine depths
   differ from the reference's (a searchsorted / denom-clamp flip of the
   ill-conditioned fine sampling, VR:239-268; tests/goldlib.py attribute_tail)
   or, with ERT, its 2048-ray chunk holds such a ray. tail_unexplained == 0;
@@ -117,6 +118,15 @@ def _check(name, prec, z, got, zall_hip, extra=None):
             "acc": _pix_err(got["acc_map"], z["out_acc_map"].reshape(n), "abs"),
             "depth": _pix_err(got["depth_map"], z["out_depth_map"].reshape(n), "depth"),
             "disp": _pix_err(got["disp_map"], zh["disp_map"].reshape(n), "disp")}
+    # disp = 1 / (depth / acc) is compared where the ray holds mass (SURVEY §8c:
+    # relative 1e-4 with acc > 1e-6); below that its value is a ratio of two
+    # near-zero sums (and NaN exactly at acc = 0), held by the acc / depth checks
+    acc_ref = z["out_acc_map"].reshape(n).astype(np.float64)
+    acc_hip = np.asarray(got["acc_map"], np.float64).reshape(n)
+    massless = (acc_ref <= 1e-6) & (acc_hip <= 1e-6)
+    e, tol = fine["disp"]
+    fine["disp"] = (np.where(massless, 0.0, e), tol)
+    nan_flip = np.isnan(zh["disp_map"].reshape(n)) != np.isnan(np.asarray(got["disp_map"]).reshape(n))
     tail = np.zeros(n, bool)
     for e, tol in fine.values():
         tail |= e > tol
@@ -145,6 +155,8 @@ def _check(name, prec, z, got, zall_hip, extra=None):
            **{f"fine_{k}_frac_within_tol": float(np.mean(e <= tol)) for k, (e, tol) in fine.items()},
            "disp_nan_ref": int(nan_ref.sum()),
            "disp_nan_hip": int(np.isnan(got["disp_map"].reshape(n)).sum()),
+           "disp_nan_flips": int(nan_flip.sum()),
+           "disp_nan_flips_with_mass": int((nan_flip & ~massless).sum()),
            "rays_with_other_fine_depths": int(ddiff.sum()),
            "tail_pixels": int(tail.sum()), "tail_unexplained": int(unexpl.sum()),
            "tail_unexplained_by_map": {k: int((unexpl & (e > tol)).sum())

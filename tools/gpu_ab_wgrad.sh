@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of a weight-gradient variant library (NERFHIP_LIB=lib/libnerfhip_<v>.so)
+# A/B of variant libraries (NERFHIP_LIB=lib/libnerfhip_<v>.so, VARIANTS="v1 v2")
 # against the tree's library: the kernel alone at the C3 fine size
 # (tools/train_kernels_bench.py) and the whole C3 step, interleaved twice.
 set -u
@@ -7,9 +7,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abw}
 mkdir -p "$OUT"
-V=${VARIANT:-wv2}
+VARIANTS=${VARIANTS:-wv2}
 for rep in 1 2; do
-  for v in base $V; do
+  for v in base $VARIANTS; do
     if [ $v = base ]; then unset NERFHIP_LIB; else export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_$v.so; fi
     echo "== $v rep $rep"
     timeout -k 10 200 python tools/train_kernels_bench.py > "$OUT/kbench_${v}_$rep.log" 2>&1 || exit $?
