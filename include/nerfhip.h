@@ -249,7 +249,10 @@ int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const int* tile_chu
  *   (nerf_x3_layer_ex's layout, m_tiles 16) for L = 0..7 and bits[8] those of
  *   the views output (m_tiles 8); amax[0..11] (device floats,
  *   caller-initialised, >= 0) are raised to max |h_0..h_7|, max |feature|,
- *   max |xyz encoding|, max |view encoding|, max |views output|. */
+ *   max |xyz encoding|, max |view encoding|, max |views output|.
+ *   act[8] may be NULL: the feature rows are then not written (the weight
+ *   gradients can be taken through h_7, nerfhip.train_mlp: dW_views,feat =
+ *   G W_feat^T + s b_feat^T with G = d_hv h_7^T). */
 typedef struct NerfX3TrainOut {
   float* act[12];
   unsigned short* bits[9];
@@ -277,13 +280,16 @@ int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float* w_head,
  *   d[0] = the gradients of the pre-activations of layers 7 .. 0 (256 rows
  *   each); with_enc also d[10] / d[11] = the xyz encoding's gradient through
  *   layer 5 / layer 0 (64 rows; row 63 is padding). io->dmax[0..8], [10]
- *   (caller-initialised, >= 0) are raised to the outputs' max |.|. */
+ *   (caller-initialised, >= 0) are raised to the outputs' max |.|. d[8] may be
+ *   NULL: d feature is then not written (dW_feat = W_views,feat^T G, see
+ *   NerfX3TrainOut). */
 typedef struct NerfX3BwdIO {
   const float* d_raw;
   const unsigned short* bits[9];
   float* d[12];
   float* dmax;
   int64_t ld;
+  float* d_raw_t;   /* nullable: d raw feature-major, rows (stride ld) d sigma, d r, d g, d b */
 } NerfX3BwdIO;
 /* nerf_mlp_forward_x3_clock: nerf_mlp_forward_x3's computation (same outputs)
  *   by a diagnostic twin of its kernel that stamps (s_memtime, s_memrealtime)

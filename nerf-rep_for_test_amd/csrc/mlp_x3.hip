@@ -365,11 +365,13 @@ struct ActStore {
   unsigned ld4;                // uniform: row stride in bytes
   unsigned wb;                 // bits of the current 4-tile block
   bool bits, valid;
+  bool on = true;              // uniform: false = these rows are not stored (null output)
   // pair G = tiles 2G (v[0..3], rows 32G + 4 g4 + r) and 2G+1 (v[4..7], rows + 16).
   // The lane's offsets are recomputed here (a few VALU in the MFMA shadows)
   // instead of living in VGPRs through the whole tile.
   template <int G>
   __device__ __forceinline__ void pair(const Op& v) {
+    if (!on) return;
     unsigned lid = __lane_id();
     asm volatile("" : "+v"(lid));
     const unsigned vo = valid ? (lid >> 4) * 4u * ld4 + (lid & 15u) * 4u + soff : 0x7fffffffu;
@@ -528,6 +530,7 @@ __device__ __forceinline__ void mlp_x3_body(
       int Li = L;
       asm volatile("" : "+s"(Li));
       st.rs = rows_rsrc(to.act[Li], rows, to.ld);
+      st.on = to.act[Li] != nullptr;   // the feature rows may be skipped (act[8] null)
       st.bits = L < 8;
       st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)to.bits[Li < 8 ? Li : 0], 0,
                                                 L < 8 ? 0x7fffffff : 0, 0x00020000);
@@ -812,6 +815,7 @@ struct X3BwdIO {
   float* d[12];                   // 0..7: D0..D7, 8: DF, 9: d_hv, 10: d_enc (layer 5), 11: (layer 0)
   float* dmax;                    // raised: [i] = max |D_i|, [8] max |DF|, [10] max |d_hv|
   int64_t ld;
+  float* d_raw_t;                 // nullable: rows 0..3 (stride ld) = d sigma, d rgb (x, y, z)
 };
 
 // Epilogue of a dgrad layer, fused into its last slice: 2^-shift * acc (exact),
@@ -983,12 +987,20 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   // (unwritten) mask words of their tile say, and no max |.| sees them
   float4 dr = io.d_raw[gl];
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (io.d_raw_t && g4 == 0 && valid) {   // d raw feature-major: the heads' wgrad operands
+    float* t = io.d_raw_t + gs;
+    t[0] = dr.w;
+    t[io.ld] = dr.x;
+    t[2 * io.ld] = dr.y;
+    t[3 * io.ld] = dr.z;
+  }
   // outputs / masks of this (tile, wave): pointers loaded at their layer
   auto store_for = [&](int k, int rows) {
     ActStore st;
     int ki = k;
     asm volatile("" : "+s"(ki));
     st.rs = rows_rsrc(io.d[ki], rows, io.ld);
+    st.on = io.d[ki] != nullptr;       // DF may be skipped (d[8] null)
     st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
     st.soff = (unsigned)((tile * kX3Tile + wave * 16) * 4);
     st.sboff = 0u;
@@ -2113,8 +2125,8 @@ extern "C" int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float
   NERF_REQUIRE(n >= 0 && S >= 1 && z_stride >= 0, "nerf_mlp_train_forward_x3: bad size");
   const int64_t P = n * S;
   NERF_REQUIRE(out->ld >= P, "nerf_mlp_train_forward_x3: bad size");
-  for (int i = 0; i < 12; ++i)
-    NERF_REQUIRE(out->act[i] != nullptr, "nerf_mlp_train_forward_x3: null output rows");
+  for (int i = 0; i < 12; ++i)   // act[8] (the feature rows) may be null: not stored
+    NERF_REQUIRE(i == 8 || out->act[i] != nullptr, "nerf_mlp_train_forward_x3: null output rows");
   for (int i = 0; i < 9; ++i)
     NERF_REQUIRE(out->bits[i] != nullptr, "nerf_mlp_train_forward_x3: null relu bits");
   NERF_REQUIRE((int64_t)256 * out->ld * 4 < (1ll << 31),
@@ -2144,8 +2156,8 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
   NERF_REQUIRE(w_slices && w_head && io && io->d_raw && io->dmax,
                "nerf_mlp_train_backward_x3: null pointer");
   NERF_REQUIRE(P >= 0 && io->ld >= P, "nerf_mlp_train_backward_x3: bad size");
-  for (int i = 0; i < 10; ++i)
-    NERF_REQUIRE(io->d[i] != nullptr, "nerf_mlp_train_backward_x3: null output rows");
+  for (int i = 0; i < 10; ++i)   // d[8] (DF) may be null: not stored
+    NERF_REQUIRE(i == 8 || io->d[i] != nullptr, "nerf_mlp_train_backward_x3: null output rows");
   if (with_enc)
     NERF_REQUIRE(io->d[10] && io->d[11], "nerf_mlp_train_backward_x3: null encoding rows");
   for (int i = 0; i < 9; ++i)
@@ -2166,6 +2178,7 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
   for (int i = 0; i < 12; ++i) b.d[i] = io->d[i];
   b.dmax = io->dmax;
   b.ld = io->ld;
+  b.d_raw_t = io->d_raw_t;
   if (with_enc)
     hipLaunchKernelGGL(mlp_x3_bwd_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
                        as_stream(stream), (const float4*)w_slices, w_head, P, b);

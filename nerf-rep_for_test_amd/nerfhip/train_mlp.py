@@ -427,7 +427,8 @@ def invalidate_packs():
 class _BwdIO(ctypes.Structure):
     """NerfX3BwdIO (include/nerfhip.h)."""
     _fields_ = [("d_raw", ctypes.c_void_p), ("bits", ctypes.c_void_p * 9),
-                ("d", ctypes.c_void_p * 12), ("dmax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
+                ("d", ctypes.c_void_p * 12), ("dmax", ctypes.c_void_p), ("ld", ctypes.c_int64),
+                ("d_raw_t", ctypes.c_void_p)]
 
 
 class _TrainOut(ctypes.Structure):
@@ -710,8 +711,8 @@ class NerfMLPFn(torch.autograd.Function):
         if not fused_f:   # (the fused forward writes the encoding rows itself)
             _encode(pts_c, XYZ_FREQS, E, amax[9:10])               # E[:63] = enc^T
             E[63].zero_()
-        H = [_act(256, P, dev) if i not in (4,) else None          # h4 rows: layer 4
-             for i in range(8)]
+        H = [_act(256, P, dev) if i not in (4, 7) or (i == 7 and not fused_f) else None
+             for i in range(8)]                      # h4 rows: E; fused: h7 rows in V
         H[4] = E[64:320]
         pk = None if fused_f and fused_b else \
             _packs_for(params, dev, forward=not fused_f, backward=not fused_b)
@@ -770,11 +771,17 @@ class NerfMLPFn(torch.autograd.Function):
         zero = _ZERO.get(str(dev))
         if zero is None:
             zero = _ZERO[str(dev)] = torch.zeros(1, device=dev, dtype=torch.float32)
+        # h7 goes into V's first 256 rows and the feature rows are not stored: the
+        # views layer's weight gradient is taken through h7 (G = d_hv [h7; enc]^T,
+        # then G W_feat^T), which also gives the feature layer's (W_views,feat^T G),
+        # so neither the feature rows nor their gradient DF ever reach HBM
+        H[7] = V[0:256]
         out = _TrainOut()
         for i in range(8):
             out.act[i] = H[i].data_ptr()
             out.bits[i] = bits[i].data_ptr()
-        out.act[8] = V[0:256].data_ptr()
+        out.act[8] = None
+        ctx.v_h7 = True
         out.act[9] = HV.data_ptr()
         out.act[10] = E[0:64].data_ptr()
         out.act[11] = V[256:288].data_ptr()
@@ -808,12 +815,22 @@ class NerfMLPFn(torch.autograd.Function):
         P = d_raw.shape[0]
         f32 = torch.float32
         grads = {}
-        # d_raw^T (the rgb / alpha heads' wgrad operands; the layer launches'
-        # d hv K step: 32 rows, 4 of them d_raw)
-        DR = torch.empty((4, P), device=dev, dtype=f32) if ctx.fused_backward else \
-            torch.zeros((32, P), device=dev, dtype=f32)
-        DR[:4].copy_(d_raw.t())
-        d_rgb, d_sig = DR[0:3], DR[3:4]
+        v_h7 = getattr(ctx, "v_h7", False)   # V = [h7; view enc] (fused forward)
+        # fused forward + backward: the alpha head's gradient rides on the views
+        # layer's G tile (A = [d_hv; d sigma], both read against [h7; enc]), so the
+        # fused backward writes d raw feature-major right behind d_hv (rows 128:
+        # d sigma, 129..131: d rgb) and no separate alpha tile re-reads h7
+        heads_merged = ctx.fused_backward and v_h7
+        if heads_merged:
+            HX = _act(132, P, dev)
+            d_sig, d_rgb = HX[128:129], HX[129:132]
+        else:
+            # d_raw^T (the rgb / alpha heads' wgrad operands; the layer launches'
+            # d hv K step: 32 rows, 4 of them d_raw)
+            DR = torch.empty((4, P), device=dev, dtype=f32) if ctx.fused_backward else \
+                torch.zeros((32, P), device=dev, dtype=f32)
+            DR[:4].copy_(d_raw.t())
+            d_rgb, d_sig = DR[0:3], DR[3:4]
         wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
         post = {}              # slot -> (weight name, bias name or None, column fix-up)
         # max |d| of each product (slots as NerfX3BwdIO.dmax); [11] / [12]: of
@@ -825,23 +842,33 @@ class NerfMLPFn(torch.autograd.Function):
         call("nerf_raw_absmax", ptr(d_raw_c), P, ptr(dmax[11:]), _lib.stream_of(dev))
         # the heads' bias gradients come out of the batched launch too (its row
         # sums), not from separate reductions over P
-        post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
-            "rgb_linear.weight", "rgb_linear.bias", None)
         rays_S = getattr(ctx, "rays_S", 0)   # RayMLPFn: the gradient goes to z [n, S]
         need_enc = ctx.pts_grad and ctx.needs_input_grad[2 if rays_S else 0]
         if ctx.fused_backward:
-            d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(d_raw_c, ctx.streams[2:], bits, bits_v,
-                                                           dmax, need_enc)
+            d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(
+                d_raw_c, ctx.streams[2:], bits, bits_v, dmax, need_enc, not v_h7,
+                HX if heads_merged else None)
         else:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
                                                             need_enc)
-        post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[8:9], amax[10:11]),
-                    with_bias=True)] = (
-            "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
-        post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
-            "feature_linear.weight", "feature_linear.bias", None)
-        post[wb.add(d_sig, H[7], dmax[12:13], amax[7:8], with_bias=True)] = (
-            "alpha_linear.weight", "alpha_linear.bias", None)
+        post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
+            "rgb_linear.weight", "rgb_linear.bias", None)
+        if heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
+            post[wb.add(HX[0:129], V, torch.maximum(dmax[10:11], dmax[12:13]),
+                        torch.maximum(amax[7:8], amax[10:11]), with_bias=True)] = (
+                "views_G", "views_GA_bias", None)
+        elif v_h7:   # G = d_hv [h7; enc]^T: both the views and the feature gradients (below)
+            post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[7:8], amax[10:11]),
+                        with_bias=True)] = ("views_G", "views_linears.0.bias", None)
+        else:
+            post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[8:9], amax[10:11]),
+                        with_bias=True)] = (
+                "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
+            post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
+                "feature_linear.weight", "feature_linear.bias", None)
+        if not heads_merged:
+            post[wb.add(d_sig, H[7], dmax[12:13], amax[7:8], with_bias=True)] = (
+                "alpha_linear.weight", "alpha_linear.bias", None)
         for i in range(7, -1, -1):
             inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
             in_max = (torch.maximum(amax[9:10], amax[4:5]) if i == 5 else
@@ -856,6 +883,24 @@ class NerfMLPFn(torch.autograd.Function):
             grads[wname] = fix(gw) if fix is not None else gw
             if bname:
                 grads[bname] = gb
+        if heads_merged:   # row 128 of the merged tile: the alpha head (NET:61 on h7)
+            GA, ba = grads.pop("views_G"), grads.pop("views_GA_bias")
+            grads["views_G"], grads["views_linears.0.bias"] = GA[:128], ba[:128]
+            grads["alpha_linear.weight"] = GA[128:129, :256]
+            grads["alpha_linear.bias"] = ba[128:129]
+        if v_h7:
+            # feature = W_f h7 + b_f (NET:63) feeds the views layer (NET:64-65), so with
+            # G = sum_p d_hv [h7; enc]^T and s = sum_p d_hv (the views bias gradient):
+            #   dW_views = [G_h7 W_f^T + s b_f^T, G_enc],  dW_f = W_vf^T G_h7,  db_f = W_vf^T s
+            G = grads.pop("views_G")
+            sv = grads["views_linears.0.bias"]
+            Gh = G[:, :256]
+            Wvf = p["views_linears.0.weight"][:, :256]
+            grads["views_linears.0.weight"] = torch.cat(
+                [torch.addmm(sv[:, None] * p["feature_linear.bias"][None, :], Gh,
+                             p["feature_linear.weight"].t()), G[:, 256:283]], 1)
+            grads["feature_linear.weight"] = Wvf.t() @ Gh
+            grads["feature_linear.bias"] = Wvf.t() @ sv
         d_pts = None
         if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
             assert d_enc[0].stride(0) == d_enc[1].stride(0)
@@ -917,11 +962,14 @@ def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
     return d_hv, DF, D, d_enc
 
 
-def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc):
+def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=True, hx=None):
     """The same chain as ONE nerf_mlp_train_backward_x3 launch over the
     transposed weight stream (X3BwdStreamPacker): every product's rows written
     feature-major and its max |.| raised, the ReLU masks from the forward's
-    bits; d_enc = the layer-5 and layer-0 encoding rows."""
+    bits; d_enc = the layer-5 and layer-0 encoding rows. store_df=False: DF is
+    not written (None; the weight gradients go through G, NerfMLPFn.backward).
+    hx: a [132, P] row buffer: d_hv goes to rows 0..127 and d raw, feature-major,
+    to rows 128..131 (d sigma, d r, d g, d b)."""
     dev = d_raw.device
     P = d_raw.shape[0]
     stream, head = streams
@@ -929,7 +977,8 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc):
     if d_raw_c.data_ptr() % 16:
         d_raw_c = d_raw_c.clone()
     D = [_act(256, P, dev) for _ in range(8)]
-    DF, d_hv = _act(256, P, dev), _act(128, P, dev)
+    DF = _act(256, P, dev) if store_df else None
+    d_hv = _act(128, P, dev) if hx is None else hx[0:128]
     de5 = _act(64, P, dev) if need_enc else None
     de0 = _act(64, P, dev) if need_enc else None
     io = _BwdIO()
@@ -938,12 +987,14 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc):
         io.bits[i] = bits[i].data_ptr()
         io.d[i] = D[i].data_ptr()
     io.bits[8] = bits_v.data_ptr()
-    io.d[8], io.d[9] = DF.data_ptr(), d_hv.data_ptr()
+    io.d[8], io.d[9] = (DF.data_ptr() if store_df else None), d_hv.data_ptr()
     io.d[10] = de5.data_ptr() if need_enc else None
     io.d[11] = de0.data_ptr() if need_enc else None
     io.dmax = dmax.data_ptr()
     io.ld = D[0].stride(0)
-    assert all(t.stride(0) == io.ld for t in [DF, d_hv] + ([de5, de0] if need_enc else []))
+    io.d_raw_t = hx[128].data_ptr() if hx is not None else None
+    assert all(t.stride(0) == io.ld for t in [d_hv] + ([DF] if store_df else []) +
+               ([de5, de0] if need_enc else []))
     call("nerf_mlp_train_backward_x3", ptr(stream), ptr(head), P, int(bool(need_enc)),
          ctypes.addressof(io), _lib.stream_of(dev))
     d_enc = (de5[:63], de0[:63]) if need_enc else None
@@ -970,8 +1021,8 @@ class RayMLPFn(torch.autograd.Function):
         dev = z.device
         E = _act(320, P, dev)
         amax = torch.zeros(12, device=dev, dtype=torch.float32)
-        H = [_act(256, P, dev) if i != 4 else None for i in range(8)]
-        H[4] = E[64:320]
+        H = [_act(256, P, dev) if i not in (4, 7) else None for i in range(8)]
+        H[4] = E[64:320]                             # h7: V's rows (_forward_fused)
         ctx.fused_backward = FUSED_BACKWARD and P > 0
         ctx.streams = _streams_for(params, dev)
         ctx.rays_S = S
