@@ -352,9 +352,12 @@ __device__ __forceinline__ void lds_max_u32(unsigned* p, unsigned v) {
 }
 
 // cache policy of the training kernels' activation / gradient row stores
-// (buffer instruction aux bits; timing A/B through `make variant`)
+// (buffer instruction aux bits): nt (2). The rows are read back by another
+// kernel after gigabytes of other traffic, never from L2; the weight stream the
+// same kernels read is. C3 3.50 vs 3.56 ms with the default policy, sc1 (16)
+// 3.67 (tools/gpu_ab_wgrad.sh, two interleaved runs each; `make variant`)
 #ifndef NERF_ACT_STORE_AUX
-#define NERF_ACT_STORE_AUX 0
+#define NERF_ACT_STORE_AUX 2
 #endif
 
 struct ActStore {
@@ -1740,89 +1743,6 @@ __device__ __forceinline__ void wgrad_dma_body(
     }
     const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
     const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
-#if NERF_WGRAD_V2
-    // Software-pipelined: the B fragments are read two tiles ahead and B tile
-    // j+1 is split inside tile j's twelve products, A tile i+1 inside A tile i's
-    // three products of tile 0 (pinned by sched_barrier: 3 MFMAs, then 2 value
-    // pairs of the next split), so no split sits right in front of the MFMAs
-    // that consume it.
-    half8 ah[4], al[4];
-    Raw ra[4], rb[3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
-    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);
-    read_pair(baseB + (unsigned)((8 * nb + 1) * 2048), rb[1]);
-    asm volatile("s_waitcnt lgkmcnt(2)"
-                 : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
-                   "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y),
-                   "+v"(rb[0].x), "+v"(rb[0].y)
-                 :
-                 : "memory");
-    Op bc = to_op(rb[0]);
-    split_op(bc, sb);
-    Op av[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      av[i] = to_op(ra[i]);
-      if (nb == 0) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) rs4[i] += av[i][t];
-      }
-    }
-    split_op(av[0], sa);
-    ah[0] = op_hi(av[0]);
-    al[0] = op_lo(av[0]);
-    // split Op v's value pairs [2q, 2q+2) in place (two split2 = 8 VALU)
-    auto split_part = [](Op& v, float sc, Op& o, int q) {
-#pragma unroll
-      for (int k = 2 * q; k < 2 * q + 2; ++k) {
-        float hp, lp;
-        split2(v[2 * k], v[2 * k + 1], sc, hp, lp);
-        o[k] = hp;
-        o[4 + k] = lp;
-      }
-    };
-    auto tile = [&](auto Jc) {
-      constexpr int j = decltype(Jc)::value;
-      const half8 bh = op_hi(bc), bl = op_lo(bc);
-      if constexpr (j + 2 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 2) * 2048), rb[(j + 2) % 3]);
-      if constexpr (j < 4) issue_piece(gb, std::integral_constant<int, j>{});
-      else issue_piece(ga, std::integral_constant<int, j - 4>{});
-      Op bn, bsplit;
-      if constexpr (j + 1 < 8) {
-        Raw& nx = rb[(j + 1) % 3];
-        if constexpr (j + 2 < 8) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(nx.x), "+v"(nx.y) : : "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(nx.x), "+v"(nx.y) : : "memory");
-        bn = to_op(nx);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
-        acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
-        acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
-        acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
-        if constexpr (j == 0) {
-          if (i + 1 < 4) {   // A tile i+1 for the next products of this tile
-            split_op(av[i + 1], sa);
-            ah[i + 1] = op_hi(av[i + 1]);
-            al[i + 1] = op_lo(av[i + 1]);
-          }
-        }
-        if constexpr (j + 1 < 8) {
-          if constexpr (j == 0) {
-            if (i == 3) {
-              split_part(bn, sb, bsplit, 0);
-              split_part(bn, sb, bsplit, 1);
-            }
-          } else if (i < 2) {
-            split_part(bn, sb, bsplit, i);
-          }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (j + 1 < 8) bc = bsplit;
-    };
-#else
     // The A fragments and the first B fragment are read together; the A split
     // runs tile by tile inside the first B tile's MFMAs (each A tile split just
     // before its own three products), so it is not a VALU-only phase at the
@@ -1867,7 +1787,6 @@ __device__ __forceinline__ void wgrad_dma_body(
         acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
       }
     };
-#endif
     tile(std::integral_constant<int, 0>{});
     tile(std::integral_constant<int, 1>{});
     tile(std::integral_constant<int, 2>{});

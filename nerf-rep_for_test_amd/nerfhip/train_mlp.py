@@ -801,7 +801,6 @@ class NerfMLPFn(torch.autograd.Function):
                  ptr(z), S, n, S, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
             # the rays' directions stand where the points do: d z = sum_c d pts_c d_c
             ctx.save_for_backward(rd, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
-            ctx.pts_grad = z.requires_grad
         ctx.packs = pk
         return raw
 
@@ -1030,6 +1029,7 @@ class RayMLPFn(torch.autograd.Function):
         rays = (rays_o.detach().contiguous(), rays_d.detach().contiguous(),
                 z.detach().contiguous())
         raw = NerfMLPFn._forward_fused(ctx, None, None, None, params, E, H, amax, pk, rays)
+        ctx.pts_grad = z.requires_grad   # (_forward_fused saw the detached copy)
         return raw.view(n, S, 4)
 
     @staticmethod

@@ -43,16 +43,25 @@ def _coarse_elem_tol(name, k):
     return max(1e-3, 2.0 * float(load("tg_" + name)["gcdist__" + k]))
 
 
+REL_FLOOR = 1e-6
+
+
 def _elementwise_grads(name, grads, coarse=False):
     """Every element of every gradient tensor against the reference's
     (tests/golden/tg_<name>.npz, make_train_fullgrad.py): per tensor the relative
     L2 distance ||g - g_ref|| / ||g_ref|| within 2x the largest distance of the
-    reference from ITSELF under exact reparametrisations (gdist / gcdist) plus a
-    floor (coarse loss 1e-4; full loss 2e-3, the norm checks' floor). A permuted,
-    sign-flipped or shifted tail of a tensor fails this, a norm check does not.
+    reference from ITSELF under exact reparametrisations (gdist / gcdist) plus
+    REL_FLOOR. A permuted, sign-flipped or shifted tail of a tensor fails this, a
+    norm check does not. Every tensor's distance is printed (and written with
+    NERF_FRAME_REPORT) next to the reference's own.
     grads: name -> tensor (None entries must have no reference gradient)."""
     tg = load("tg_" + name)
-    key, dkey, floor = ("gc__", "gcdist__", 1e-4) if coarse else ("g__", "gdist__", 2e-3)
+    # the bound is the reference's own distance from itself, tensor by tensor (plus
+    # 1e-6 of float32 summation noise for tensors the reparametrisations leave
+    # bitwise unchanged); round 3's fixed floors (1e-4 coarse, 2e-3 full) set the
+    # bound for most tensors and were retired once the measured distances showed
+    # every tensor within 2x the reference's own (gpurun_out report, DESIGN §6)
+    key, dkey, floor = ("gc__", "gcdist__", REL_FLOOR) if coarse else ("g__", "gdist__", REL_FLOOR)
     worst = {}
     for k, g in grads.items():
         if key + k not in tg:
