@@ -134,14 +134,25 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 /* nerf_sum_partials: out[i] = sum_{c=0}^{C-1} part[c * n + i], summed in c
  *   order (the weight-gradient split-K partials of nerf_x3_wgrad). */
 int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream);
+/* The views / feature / alpha weight gradients of the lego NeRF (NET:61-65)
+ * from GA = [d_hv; d sigma] [h7; view enc]^T ([129][288+], row stride ldga) and
+ * its row sums ba[129] (nerfhip.train_mlp): dWv [128][283] = [Gh W_f^T + s b_f^T,
+ * GA[0:128, 256:283]], dWf [256][256] = W_v[:, :256]^T Gh, dbf [256] =
+ * W_v[:, :256]^T s, dWa [256] = GA[128, 0:256], dba [1] = ba[128], dbv [128] =
+ * s (Gh = GA[0:128, 0:256], s = ba[0:128]; W_f [256][256], b_f [256],
+ * W_v [128][283] row-major). */
+int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, const float* Wf,
+                             const float* bf, const float* Wv, float* dWv, float* dWf, float* dbf,
+                             float* dWa, float* dba, float* dbv, nerf_stream_t stream);
 /* trainers/nerf.py:39-76: out[0] = mean((a - target)^2), out[1] = the same of b
  * (0 when b is NULL), out[2] = out[0] + out[1] (a, b, target: N floats; one
- * workgroup). Backward: g[3] = d out; da = (2/N)(a - t)(g[0] + g[2]), db =
- * (2/N)(b - t)(g[1] + g[2]). */
+ * workgroup). Backward: g0, g1, g2 = d out[0..2] (device scalars, each nullable
+ * = 0); da = (2/N)(a - t)(g0 + g2), db = (2/N)(b - t)(g1 + g2). */
 int nerf_mse_pair(const float* a, const float* b, const float* target, int64_t N, float* out,
                   nerf_stream_t stream);
 int nerf_mse_pair_backward(const float* a, const float* b, const float* target, int64_t N,
-                           const float* g, float* da, float* db, nerf_stream_t stream);
+                           const float* g0, const float* g1, const float* g2, float* da,
+                           float* db, nerf_stream_t stream);
 int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
                         const float* g_zall, int64_t n, int S, int n_imp,
                         float* d_weights, nerf_stream_t stream);
@@ -226,6 +237,8 @@ typedef struct NerfWgradDesc {
   float* bias_part;
   int64_t ldbias;
   int M, N;
+  const float* amax_a2;   /* nullable: the A scale covers max(*amax_a, *amax_a2) */
+  const float* amax_b2;   /* nullable: likewise for B */
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
 /* The same with a K split per output tile: tile_chunks[t] (1 .. zmax, < 256)

@@ -1664,8 +1664,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 constexpr int kWgRing = 5;
 __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
-    const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float* __restrict__ amax_a,
-    const float* __restrict__ amax_b, float* __restrict__ part, int64_t ldpart,
+    const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
+    const float amax_b, float* __restrict__ part, int64_t ldpart,
     float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1674,7 +1674,7 @@ __device__ __forceinline__ void wgrad_dma_body(
   const int64_t pb = (int64_t)z * 32, kstride = (int64_t)Z * 32;
   const int nsteps = pb < P ? (int)((P - pb + kstride - 1) / kstride) : 0;
   const int ngran = 2 * nsteps;
-  const int ea = act_exponent(*amax_a), eb = act_exponent(*amax_b);
+  const int ea = act_exponent(amax_a), eb = act_exponent(amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
 
   // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1)
@@ -1827,7 +1827,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
     int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
     float* __restrict__ part, float* __restrict__ bias_part) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
-  wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, amax_a, amax_b, part, (int64_t)M * N, bias_part,
+  wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, *amax_a, *amax_b, part, (int64_t)M * N, bias_part,
                  M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z);
 }
 
@@ -1857,7 +1857,10 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
   const int z = w - (bt.t_wg_end[t] - Z);
   const NerfWgradDesc& d = bt.d[bt.t_desc[t]];
   const int mtile = bt.t_m[t], ntile = bt.t_n[t];
-  wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, d.amax_a, d.amax_b, d.part,
+  // a scale may cover two tensors' maxima (rows of two producers in one operand)
+  const float ma = d.amax_a2 ? fmaxf(*d.amax_a, *d.amax_a2) : *d.amax_a;
+  const float mb = d.amax_b2 ? fmaxf(*d.amax_b, *d.amax_b2) : *d.amax_b;
+  wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, ma, mb, d.part,
                  d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z);
   if (z != 0 || Z >= bt.Zmax) return;
   // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)

@@ -402,14 +402,17 @@ __global__ __launch_bounds__(kMseThreads) void mse_pair_kernel(const float* __re
 __global__ __launch_bounds__(256) void mse_pair_bwd_kernel(const float* __restrict__ a,
                                                            const float* __restrict__ b,
                                                            const float* __restrict__ t, int64_t N,
-                                                           const float* __restrict__ g,
+                                                           const float* __restrict__ g0,
+                                                           const float* __restrict__ g1,
+                                                           const float* __restrict__ g2,
                                                            float* __restrict__ da,
                                                            float* __restrict__ db) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const float norm = 2.0f / (float)N;
-  // g: d loss_c, d loss_f, d (loss_c + loss_f)
-  const float gc = g[0] + g[2], gf = g[1] + g[2];
+  // d loss_c, d loss_f, d (loss_c + loss_f); a null gradient is 0
+  const float l = g2 ? *g2 : 0.0f;
+  const float gc = g0 ? *g0 + l : l, gf = g1 ? *g1 + l : l;
   da[i] = norm * (a[i] - t[i]) * gc;
   if (b) db[i] = norm * (b[i] - t[i]) * gf;
 }
@@ -425,10 +428,11 @@ int nerf_mse_pair(const float* a, const float* b, const float* target, int64_t N
 }
 
 int nerf_mse_pair_backward(const float* a, const float* b, const float* target, int64_t N,
-                           const float* g, float* da, float* db, nerf_stream_t stream) {
-  NERF_REQUIRE(a && target && g && da && (!b || db) && N > 0, "nerf_mse_pair_backward: bad arguments");
+                           const float* g0, const float* g1, const float* g2, float* da,
+                           float* db, nerf_stream_t stream) {
+  NERF_REQUIRE(a && target && da && (!b || db) && N > 0, "nerf_mse_pair_backward: bad arguments");
   hipLaunchKernelGGL(mse_pair_bwd_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0,
-                     as_stream(stream), a, b, target, N, g, da, db);
+                     as_stream(stream), a, b, target, N, g0, g1, g2, da, db);
   return check_launch("mse_pair_bwd_kernel");
 }
 
@@ -498,6 +502,77 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
   }
   for (; c < C; ++c) s += p[c * n];
   out[i] = s;
+}
+
+// The views / feature / alpha weight gradients from the merged G tile of the
+// batched weight-gradient launch (nerfhip.train_mlp, NET:61-65): GA = [d_hv;
+// d sigma] [h7; view enc]^T ([129][288], row stride ldga), ba = its row sums
+// ([129]); feature = W_f h7 + b_f feeds the views layer, so with Gh = GA[0:128,
+// 0:256] and s = ba[0:128]:
+//   dW_views = [Gh W_f^T + s b_f^T, GA[0:128, 256:283]],  db_views = s,
+//   dW_f = W_views[:, :256]^T Gh,  db_f = W_views[:, :256]^T s,
+//   dW_alpha = GA[128, 0:256],  db_alpha = ba[128].
+// One thread per output element, float32 sums in k order (one launch in place
+// of two small hipBLASLt GEMMs, a GEMV and the copies around them).
+constexpr int kVfViews = 128 * 283, kVfFeat = 256 * 256;
+constexpr int kVfTotal = kVfViews + kVfFeat + 256 + 256 + 1 + 128;
+__global__ __launch_bounds__(256) void views_feature_grads_kernel(
+    const float* __restrict__ GA, int64_t ldga, const float* __restrict__ ba,
+    const float* __restrict__ Wf, const float* __restrict__ bf, const float* __restrict__ Wv,
+    float* __restrict__ dWv, float* __restrict__ dWf, float* __restrict__ dbf,
+    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv) {
+  int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= kVfTotal) return;
+  if (t < kVfViews) {
+    const int i = t / 283, j = t % 283;
+    const float* g = GA + (int64_t)i * ldga;
+    if (j >= 256) {
+      dWv[t] = g[j];
+      return;
+    }
+    const float* w = Wf + (int64_t)j * 256;
+    float acc = 0.0f;
+    for (int k = 0; k < 256; ++k) acc = __builtin_fmaf(g[k], w[k], acc);
+    dWv[t] = __builtin_fmaf(ba[i], bf[j], acc);
+    return;
+  }
+  t -= kVfViews;
+  if (t < kVfFeat) {
+    const int a = t >> 8, b = t & 255;
+    float acc = 0.0f;
+    for (int i = 0; i < 128; ++i)
+      acc = __builtin_fmaf(Wv[(int64_t)i * 283 + a], GA[(int64_t)i * ldga + b], acc);
+    dWf[t] = acc;
+    return;
+  }
+  t -= kVfFeat;
+  if (t < 256) {
+    float acc = 0.0f;
+    for (int i = 0; i < 128; ++i) acc = __builtin_fmaf(Wv[(int64_t)i * 283 + t], ba[i], acc);
+    dbf[t] = acc;
+    return;
+  }
+  t -= 256;
+  if (t < 256) {
+    dWa[t] = GA[128 * ldga + t];
+    return;
+  }
+  t -= 256;
+  if (t == 0) {
+    dba[0] = ba[128];
+    return;
+  }
+  dbv[t - 1] = ba[t - 1];
+}
+
+int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, const float* Wf,
+                             const float* bf, const float* Wv, float* dWv, float* dWf, float* dbf,
+                             float* dWa, float* dba, float* dbv, nerf_stream_t stream) {
+  NERF_REQUIRE(GA && ba && Wf && bf && Wv && dWv && dWf && dbf && dWa && dba && dbv && ldga >= 283,
+               "nerf_views_feature_grads: bad arguments");
+  hipLaunchKernelGGL(views_feature_grads_kernel, dim3((unsigned)cdiv(kVfTotal, 256)), dim3(256), 0,
+                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv);
+  return check_launch("views_feature_grads_kernel");
 }
 
 int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream) {

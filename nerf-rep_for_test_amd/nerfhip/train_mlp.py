@@ -526,7 +526,8 @@ class _WgradDesc(ctypes.Structure):
                 ("ldb", ctypes.c_int64), ("P", ctypes.c_int64), ("amax_a", ctypes.c_void_p),
                 ("amax_b", ctypes.c_void_p), ("part", ctypes.c_void_p),
                 ("ldpart", ctypes.c_int64), ("bias_part", ctypes.c_void_p),
-                ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int)]
+                ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int),
+                ("amax_a2", ctypes.c_void_p), ("amax_b2", ctypes.c_void_p)]
 
 
 _NCU = {}
@@ -608,7 +609,8 @@ class WgradBatch:
                   and A.numel() * 4 < (1 << 31) and B.numel() * 4 < (1 << 31)
                   for A, B, *_ in req))
         if not ok:
-            return [_wgrad(A, B, aa, ab, wb) for A, B, aa, ab, wb in req]
+            one = lambda m: torch.maximum(*m) if isinstance(m, tuple) else m   # noqa: E731
+            return [_wgrad(A, B, one(aa), one(ab), wb) for A, B, aa, ab, wb in req]
         zs = wgrad_tile_chunks([(A.shape[0], B.shape[0]) for A, B, *_ in req], P, _n_cu(self.device))
         Z = max(zs)
         sizes = [A.shape[0] * B.shape[0] for A, B, *_ in req]
@@ -618,11 +620,14 @@ class WgradBatch:
         bpart = torch.empty((Z, ldb), device=self.device, dtype=torch.float32)
         descs = (_WgradDesc * len(req))()
         off = boff = 0
+        def two(m):   # a scale given as (tensor, tensor): the kernel takes their max
+            return (m[0].data_ptr(), m[1].data_ptr()) if isinstance(m, tuple) else (m.data_ptr(), None)
         for k, (A, B, aa, ab, wb) in enumerate(req):
+            (a1, a2), (b1, b2) = two(aa), two(ab)
             descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
-                                  aa.data_ptr(), ab.data_ptr(), part.data_ptr() + 4 * off, ld,
+                                  a1, b1, part.data_ptr() + 4 * off, ld,
                                   bpart.data_ptr() + 4 * boff if wb else None, ldb,
-                                  A.shape[0], B.shape[0])
+                                  A.shape[0], B.shape[0], a2, b2)
             off += sizes[k]
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
@@ -853,14 +858,14 @@ class NerfMLPFn(torch.autograd.Function):
         post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
         if heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
-            post[wb.add(HX[0:129], V, torch.maximum(dmax[10:11], dmax[12:13]),
-                        torch.maximum(amax[7:8], amax[10:11]), with_bias=True)] = (
+            post[wb.add(HX[0:129], V, (dmax[10:11], dmax[12:13]),
+                        (amax[7:8], amax[10:11]), with_bias=True)] = (
                 "views_G", "views_GA_bias", None)
         elif v_h7:   # G = d_hv [h7; enc]^T: both the views and the feature gradients (below)
-            post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[7:8], amax[10:11]),
+            post[wb.add(d_hv, V, dmax[10:11], (amax[7:8], amax[10:11]),
                         with_bias=True)] = ("views_G", "views_linears.0.bias", None)
         else:
-            post[wb.add(d_hv, V, dmax[10:11], torch.maximum(amax[8:9], amax[10:11]),
+            post[wb.add(d_hv, V, dmax[10:11], (amax[8:9], amax[10:11]),
                         with_bias=True)] = (
                 "views_linears.0.weight", "views_linears.0.bias", lambda g: g[:, :283])
             post[wb.add(DF, H[7], dmax[8:9], amax[7:8], with_bias=True)] = (
@@ -870,7 +875,7 @@ class NerfMLPFn(torch.autograd.Function):
                 "alpha_linear.weight", "alpha_linear.bias", None)
         for i in range(7, -1, -1):
             inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
-            in_max = (torch.maximum(amax[9:10], amax[4:5]) if i == 5 else
+            in_max = ((amax[9:10], amax[4:5]) if i == 5 else
                       amax[9:10] if i == 0 else amax[i - 1:i])
             fix = ((lambda g: g[:, :63]) if i == 0 else
                    (lambda g: torch.cat([g[:, :63], g[:, 64:320]], 1)) if i == 5 else None)
@@ -882,12 +887,22 @@ class NerfMLPFn(torch.autograd.Function):
             grads[wname] = fix(gw) if fix is not None else gw
             if bname:
                 grads[bname] = gb
-        if heads_merged:   # row 128 of the merged tile: the alpha head (NET:61 on h7)
+        if heads_merged:   # the views / feature / alpha gradients in one launch (below)
             GA, ba = grads.pop("views_G"), grads.pop("views_GA_bias")
-            grads["views_G"], grads["views_linears.0.bias"] = GA[:128], ba[:128]
-            grads["alpha_linear.weight"] = GA[128:129, :256]
-            grads["alpha_linear.bias"] = ba[128:129]
-        if v_h7:
+            for n, shape in (("views_linears.0.weight", (128, 283)),
+                             ("feature_linear.weight", (256, 256)),
+                             ("feature_linear.bias", (256,)), ("alpha_linear.weight", (1, 256)),
+                             ("alpha_linear.bias", (1,)), ("views_linears.0.bias", (128,))):
+                grads[n] = torch.empty(shape, device=dev, dtype=f32)
+            Wf, bf, Wv = (p["feature_linear.weight"].detach().contiguous(),
+                          p["feature_linear.bias"].detach().contiguous(),
+                          p["views_linears.0.weight"].detach().contiguous())
+            call("nerf_views_feature_grads", ptr(GA), GA.stride(0), ptr(ba), ptr(Wf), ptr(bf),
+                 ptr(Wv), ptr(grads["views_linears.0.weight"]), ptr(grads["feature_linear.weight"]),
+                 ptr(grads["feature_linear.bias"]), ptr(grads["alpha_linear.weight"]),
+                 ptr(grads["alpha_linear.bias"]), ptr(grads["views_linears.0.bias"]),
+                 _lib.stream_of(dev))
+        elif v_h7:
             # feature = W_f h7 + b_f (NET:63) feeds the views layer (NET:64-65), so with
             # G = sum_p d_hv [h7; enc]^T and s = sum_p d_hv (the views bias gradient):
             #   dW_views = [G_h7 W_f^T + s b_f^T, G_enc],  dW_f = W_vf^T G_h7,  db_f = W_vf^T s

@@ -110,17 +110,17 @@ class MSEPairFn(torch.autograd.Function):
              _lib.stream_of(a.device))
         ctx.save_for_backward(a_c, b_c, t_c)
         ctx.has_b = b is not None
+        ctx.set_materialize_grads(False)   # unused outputs' gradients stay None (= 0)
         return out[0], out[1], out[2]
 
     @staticmethod
     def backward(ctx, g0, g1, g2):
         a, b, t = ctx.saved_tensors
-        g = torch.stack([x if x is not None else torch.zeros((), device=a.device)
-                         for x in (g0, g1, g2)]).to(torch.float32).contiguous()
+        gs = [None if x is None else x.to(torch.float32).contiguous() for x in (g0, g1, g2)]
         da = torch.empty_like(a)
         db = torch.empty_like(b) if ctx.has_b else None
-        call("nerf_mse_pair_backward", ptr(a), ptr(b), ptr(t), a.numel(), ptr(g), ptr(da),
-             ptr(db), _lib.stream_of(a.device))
+        call("nerf_mse_pair_backward", ptr(a), ptr(b), ptr(t), a.numel(), *[ptr(x) for x in gs],
+             ptr(da), ptr(db), _lib.stream_of(a.device))
         return da, db, None
 
 

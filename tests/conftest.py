@@ -16,8 +16,10 @@ def pytest_configure(config):
 
 
 def golden_names(prefix=""):
+    """The crop fixtures f<digit>..._<name>.npz (not the whole-frame companions)."""
+    import re
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.startswith("f") and f.endswith(".npz") and f.startswith(prefix))
+                  if re.match(r"f\d", f) and f.endswith(".npz") and f.startswith(prefix))
 
 
 @pytest.fixture(scope="session")

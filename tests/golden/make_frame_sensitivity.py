@@ -23,7 +23,7 @@ its seed in the reference's chunk order (VR:233-234). The unpermuted network
 reproduces the stored maps of these pixels bit for bit (asserted), which pins
 the subset rendering.
 
-Outputs ``tests/golden/fs_<frame>.npz``: ``pixels`` (int32), ``spread_<map>``
+Outputs ``tests/golden/rs_<frame>.npz``: ``pixels`` (int32), ``spread_<map>``
 (float32 per pixel, NaN-aware), ``variant_frac_ok``. Only numbers are stored.
 
     python tests/golden/make_frame_sensitivity.py [r0_c2_frame0 r1_c2_frame8_pert]
@@ -159,7 +159,7 @@ def main(argv):
             frac_ok.append(float(ok.mean()))
             print(f"{name} variant {v}: {time.time() - t0:.0f} s, within 1e-5 {ok.mean():.4f}",
                   flush=True)
-        np.savez_compressed(os.path.join(MRF.OUT, "fs_" + name + ".npz"), pixels=pix,
+        np.savez_compressed(os.path.join(MRF.OUT, "rs_" + name + ".npz"), pixels=pix,
                             variant_frac_ok=np.array(frac_ok), k_variants=K_VARIANTS,
                             ckpt_sha256=MRF.ckpt_sha(),
                             **{"spread_" + k: v.astype(np.float32) for k, v in spread.items()})
