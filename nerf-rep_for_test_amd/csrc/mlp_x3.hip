@@ -1917,8 +1917,12 @@ __global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __r
   const int per = (total + kPackSlabs - 1) / kPackSlabs;
   const int i0 = blockIdx.y * per, i1 = min(total, i0 + per);
   float mx = 0.0f;
+  // the max is order-free: walk the source along its contiguous index (a
+  // transposed pack reads W column by column otherwise: one line per element)
+  const bool by_row = d.ldc > d.ldr;
   for (int idx = i0 + (int)threadIdx.x; idx < i1; idx += 256) {
-    const int ri = d.rowmap[idx / d.K], ck = d.colmap[idx % d.K];
+    const int a = by_row ? idx % d.M : idx / d.K, c = by_row ? idx / d.M : idx % d.K;
+    const int ri = d.rowmap[a], ck = d.colmap[c];
     if (ri >= 0 && ck >= 0) mx = fmaxf(mx, fabsf(d.src[ri * d.ldr + ck * d.ldc]));
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));

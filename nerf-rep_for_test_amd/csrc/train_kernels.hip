@@ -513,14 +513,15 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 //   dW_f = W_views[:, :256]^T Gh,  db_f = W_views[:, :256]^T s,
 //   dW_alpha = GA[128, 0:256],  db_alpha = ba[128].
 // One thread per output element, float32 sums in k order (one launch in place
-// of two small hipBLASLt GEMMs, a GEMV and the copies around them).
+// of two small hipBLASLt GEMMs, a GEMV and the copies around them); vec: GA's
+// rows and W_f 16-B aligned.
 constexpr int kVfViews = 128 * 283, kVfFeat = 256 * 256;
 constexpr int kVfTotal = kVfViews + kVfFeat + 256 + 256 + 1 + 128;
 __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     const float* __restrict__ GA, int64_t ldga, const float* __restrict__ ba,
     const float* __restrict__ Wf, const float* __restrict__ bf, const float* __restrict__ Wv,
     float* __restrict__ dWv, float* __restrict__ dWf, float* __restrict__ dbf,
-    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv) {
+    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv, bool vec) {
   int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (t >= kVfTotal) return;
   if (t < kVfViews) {
@@ -532,7 +533,20 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     }
     const float* w = Wf + (int64_t)j * 256;
     float acc = 0.0f;
-    for (int k = 0; k < 256; ++k) acc = __builtin_fmaf(g[k], w[k], acc);
+    if (vec) {   // 16-B loads (4 k per load; the lanes' W_f rows are 1 KiB apart)
+      const float4* g4 = reinterpret_cast<const float4*>(g);
+      const float4* w4 = reinterpret_cast<const float4*>(w);
+#pragma unroll 4
+      for (int k = 0; k < 64; ++k) {
+        const float4 a = g4[k], b = w4[k];
+        acc = __builtin_fmaf(a.x, b.x, acc);
+        acc = __builtin_fmaf(a.y, b.y, acc);
+        acc = __builtin_fmaf(a.z, b.z, acc);
+        acc = __builtin_fmaf(a.w, b.w, acc);
+      }
+    } else {
+      for (int k = 0; k < 256; ++k) acc = __builtin_fmaf(g[k], w[k], acc);
+    }
     dWv[t] = __builtin_fmaf(ba[i], bf[j], acc);
     return;
   }
@@ -571,7 +585,8 @@ int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, con
   NERF_REQUIRE(GA && ba && Wf && bf && Wv && dWv && dWf && dbf && dWa && dba && dbv && ldga >= 283,
                "nerf_views_feature_grads: bad arguments");
   hipLaunchKernelGGL(views_feature_grads_kernel, dim3((unsigned)cdiv(kVfTotal, 256)), dim3(256), 0,
-                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv);
+                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv,
+                     ((uintptr_t)GA | (uintptr_t)Wf | (uintptr_t)(ldga * 4)) % 16 == 0);
   return check_launch("views_feature_grads_kernel");
 }
 
@@ -601,14 +616,18 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 // the last workgroup to finish writes step = t (every workgroup read the old
 // count first).
 constexpr int kAdamMax = 64;
-constexpr int kAdamBlock = 4096;   // elements per workgroup (a few hundred workgroups:
-                                   // as many atomics on the finish counter)
+constexpr int kAdamPer = 4;                 // elements per thread, loaded together
+constexpr int kAdamBlock = 256 * kAdamPer;  // elements per workgroup (~1 200 workgroups for
+                                            // both networks: as many finish-counter atomics)
 struct AdamBatch {
   NerfAdamTensor t[kAdamMax];
   int blk_end[kAdamMax];           // prefix sums of the tensors' workgroups
   int nt;
 };
 
+// Every load of a thread is issued before any of its stores (the tensors are
+// distinct arrays, declared so): one HBM latency per thread instead of one per
+// element, which a loop with a store between dependent loads would expose.
 __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const float* __restrict__ lr,
                                                    float* __restrict__ step,
                                                    unsigned* __restrict__ done, double beta1,
@@ -618,32 +637,41 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const floa
   while (k + 1 < b.nt && blk >= b.blk_end[k]) ++k;
   const NerfAdamTensor& T = b.t[k];
   const int64_t base = (int64_t)(blk - (k ? b.blk_end[k - 1] : 0)) * kAdamBlock;
-  __shared__ float coef[3];
-  if (threadIdx.x == 0) {   // the bias corrections once per workgroup (double, as torch's scalars)
-    const float t = *step + 1.0f;
-    coef[0] = (float)((double)*lr / (1.0 - pow(beta1, (double)t)));
-    coef[1] = (float)sqrt(1.0 - pow(beta2, (double)t));
-    coef[2] = t;
-  }
-  __syncthreads();
-  const float step_size = coef[0], bc2s = coef[1], t = coef[2];
+  float* __restrict__ P = T.p;
+  float* __restrict__ G = T.g;
+  float* __restrict__ M = T.m;
+  float* __restrict__ V = T.v;
+  // the bias corrections in double, as torch's Python scalars (every thread: no
+  // LDS round trip and barrier in front of the loads)
+  const float t = *step + 1.0f;
+  const float step_size = (float)((double)*lr / (1.0 - pow(beta1, (double)t)));
+  const float bc2s = (float)sqrt(1.0 - pow(beta2, (double)t));
   const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2), b2 = (float)beta2;
+  float g[kAdamPer], m0[kAdamPer], v0[kAdamPer], p0[kAdamPer];
 #pragma unroll
-  for (int r = 0; r < kAdamBlock / 256; ++r) {
+  for (int r = 0; r < kAdamPer; ++r) {
+    const int64_t i = base + r * 256 + threadIdx.x;
+    const bool in = i < T.n;
+    g[r] = in ? G[i] : 0.0f;
+    m0[r] = in ? M[i] : 0.0f;
+    v0[r] = in ? V[i] : 0.0f;
+    p0[r] = in ? P[i] : 0.0f;
+  }
+#pragma unroll
+  for (int r = 0; r < kAdamPer; ++r) {
     const int64_t i = base + r * 256 + threadIdx.x;
     if (i < T.n) {
-      float g = T.g[i];
+      float gr = g[r];
       if (clip >= 0.0f) {   // torch.clamp keeps a NaN (fminf/fmaxf would drop it)
-        g = (g != g) ? g : fminf(fmaxf(g, -clip), clip);
-        T.g[i] = g;
+        gr = (gr != gr) ? gr : fminf(fmaxf(gr, -clip), clip);
+        G[i] = gr;
       }
-      const float m0 = T.m[i];
-      const float m = m0 + w1 * (g - m0);               // lerp (weight < 0.5)
-      const float v = T.v[i] * b2 + (w2 * g) * g;        // mul_, addcmul_
-      T.m[i] = m;
-      T.v[i] = v;
+      const float m = m0[r] + w1 * (gr - m0[r]);          // lerp (weight < 0.5)
+      const float v = v0[r] * b2 + (w2 * gr) * gr;        // mul_, addcmul_
+      M[i] = m;
+      V[i] = v;
       const float denom = sqrtf(v) / bc2s + eps;
-      T.p[i] = T.p[i] + (-step_size) * (m / denom);     // addcdiv_
+      P[i] = p0[r] + (-step_size) * (m / denom);          // addcdiv_
     }
   }
   __syncthreads();   // this workgroup's reads of *step are done
