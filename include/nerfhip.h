@@ -117,10 +117,11 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
 /* nerf_adam_step: one Adam step (torch.optim.Adam with weight_decay 0, no
  *   amsgrad; trainers/trainer.py's optimizer) over n <= 64 parameter tensors in
  *   ONE launch, each gradient first clamped in place to [-clip, clip]
- *   (clip_grad_value_, trainer.py:59; clip <= 0: no clamp). tensors: host
- *   array {p, g, m (exp_avg), v (exp_avg_sq), n} (device float pointers).
- *   lr, step: device floats (the step count before this step; the launch
- *   leaves step + 1); done: a device u32, 0 between launches. */
+ *   (clip_grad_value_, trainer.py:59; NaN kept; clip < 0: no clamp). tensors:
+ *   host array {p, g, m (exp_avg), v (exp_avg_sq), n} (device float pointers).
+ *   lr, step: device floats (the step count before this step; a second tiny
+ *   launch on the stream leaves step + 1); done: unused (kept for the ABI,
+ *   may be NULL). */
 typedef struct NerfAdamTensor {
   float* p;
   float* g;
@@ -239,6 +240,9 @@ typedef struct NerfWgradDesc {
   int M, N;
   const float* amax_a2;   /* nullable: the A scale covers max(*amax_a, *amax_a2) */
   const float* amax_b2;   /* nullable: likewise for B */
+  int64_t ldo;            /* row stride of the partials ([M][ldo] at part + z * ldpart);
+                             0: N. Two descriptors with the same A can write the column
+                             blocks of one gradient (the skip layer's [enc | h4]) */
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
 /* The same with a K split per output tile: tile_chunks[t] (1 .. zmax, < 256)

@@ -538,8 +538,8 @@ __device__ __forceinline__ void mlp_x3_body(
       st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)to.bits[Li < 8 ? Li : 0], 0,
                                                 L < 8 ? 0x7fffffff : 0, 0x00020000);
       st.soff = (unsigned)((tile * kX3Tile + wv * 16) * 4);
-      st.sboff = (unsigned)(((tile * 8 + wv) * 4) * 64 * 2);
       st.ld4 = (unsigned)(to.ld * 4);
+      st.sboff = (unsigned)(((tile * 8 + wv) * 4) * 64 * 2);
       st.wb = 0u;
       st.valid = valid;
     } else {
@@ -1006,8 +1006,8 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     st.on = io.d[ki] != nullptr;       // DF may be skipped (d[8] null)
     st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
     st.soff = (unsigned)((tile * kX3Tile + wave * 16) * 4);
-    st.sboff = 0u;
     st.ld4 = (unsigned)(io.ld * 4);
+    st.sboff = 0u;
     st.wb = 0u;
     st.bits = false;
     st.valid = valid;
@@ -1666,7 +1666,8 @@ __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
     const float amax_b, float* __restrict__ part, int64_t ldpart,
-    float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z) {
+    float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z,
+    int64_t ldo) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
@@ -1694,7 +1695,8 @@ __device__ __forceinline__ void wgrad_dma_body(
   auto issue_piece = [&](int g, auto Ic) {
     constexpr int I = decltype(Ic)::value;
     if (g >= ngran) return;
-    const int so = __builtin_amdgcn_readfirstlane((int)((pb + (int64_t)(g >> 1) * kstride) * 4));
+    const int64_t p0 = pb + (int64_t)(g >> 1) * kstride;
+    const int so = __builtin_amdgcn_readfirstlane((int)(p0 * 4));
     uint4* dst = &ring[g % kWgRing][(4 * wave + I) * 64];
     if (g & 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_ptr_t)dst, 16, (int)voB[I], so, 0, 0);
     else __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)dst, 16, (int)voA[I], so, 0, 0);
@@ -1818,7 +1820,7 @@ __device__ __forceinline__ void wgrad_dma_body(
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + 64 * mb + 16 * i + 4 * g4 + r;
         const int n = n0 + 128 * nb + 16 * j + (lane & 15);
-        if (m < M && n < N) out[(int64_t)m * N + n] = acc[i][j][r] * inv;
+        if (m < M && n < N) out[(int64_t)m * ldo + n] = acc[i][j][r] * inv;
       }
 }
 
@@ -1828,7 +1830,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
     float* __restrict__ part, float* __restrict__ bias_part) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
   wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, *amax_a, *amax_b, part, (int64_t)M * N, bias_part,
-                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z);
+                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, N);
 }
 
 // Several weight gradients in one launch (the whole backward of a network):
@@ -1860,8 +1862,9 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
   // a scale may cover two tensors' maxima (rows of two producers in one operand)
   const float ma = d.amax_a2 ? fmaxf(*d.amax_a, *d.amax_a2) : *d.amax_a;
   const float mb = d.amax_b2 ? fmaxf(*d.amax_b, *d.amax_b2) : *d.amax_b;
+  const int64_t ldo = d.ldo ? d.ldo : d.N;
   wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, ma, mb, d.part,
-                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z);
+                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z, ldo);
   if (z != 0 || Z >= bt.Zmax) return;
   // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)
   const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
@@ -1870,7 +1873,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
     float* out = d.part + (int64_t)zz * d.ldpart;
     for (int i = threadIdx.x; i < rows * cols; i += kTrainThreads) {
       const int m = m0 + i / cols, n = n0 + i % cols;
-      out[(int64_t)m * d.N + n] = 0.0f;
+      out[(int64_t)m * ldo + n] = 0.0f;
     }
     if (d.bias_part && ntile == 0)
       for (int i = threadIdx.x; i < rows; i += kTrainThreads)
@@ -2256,8 +2259,10 @@ extern "C" int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const in
   int nt = 0, wgs = 0;
   for (int k = 0; k < n; ++k) {
     const NerfWgradDesc& d = descs[k];
+    const int64_t ldo = d.ldo ? d.ldo : d.N;
     NERF_REQUIRE(d.A && d.B && d.amax_a && d.amax_b && d.part && d.M > 0 && d.N > 0 &&
-                     d.P >= 0 && d.lda >= d.P && d.ldb >= d.P && d.ldpart >= (int64_t)d.M * d.N &&
+                     d.P >= 0 && d.lda >= d.P && d.ldb >= d.P && ldo >= d.N &&
+                     d.ldpart >= (int64_t)(d.M - 1) * ldo + d.N &&
                      (!d.bias_part || d.ldbias >= d.M),
                  "nerf_x3_wgrad_batch: bad descriptor");
     NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P),

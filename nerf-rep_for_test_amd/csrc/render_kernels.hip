@@ -613,22 +613,49 @@ __global__ __launch_bounds__(64 * FINE_WAVES) void sample_fine_kernel(
   const unsigned long long bal = __ballot(unsorted);
   const bool sorted_in_place = ((bal >> (lane & ~(FINE_LANES - 1))) & 0xffffull) == 0;
   if (!sorted_in_place) {
-    for (int k = 2; k <= p2; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int i = t; i < p2; i += FINE_LANES) {
-          const int prt = i ^ jj;
-          if (prt > i) {
-            const float a = zf[i], b = zf[prt];
-            const bool up = (i & k) == 0;
-            if ((a > b) == up) { zf[i] = b; zf[prt] = a; }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
+    // bitonic sort in registers: element i = t + 16 q is x[q] of lane t (q <
+    // p2 / 16 <= QN; inf past n_imp); partners 16 apart or more sit in the same
+    // lane (a register pair), closer ones in the lane group (a shuffle). The
+    // sorted values are unique, so any correct network gives the LDS sort's
+    // result; this one keeps every step in registers (training: random u, no
+    // sorted rows; the LDS version spent ~28 dependent LDS passes per ray here).
+    const int nr = p2 / FINE_LANES;
 #pragma unroll
     for (int q = 0; q < QN; ++q)
-      if (q < nq) x[q] = zf[t + FINE_LANES * q];
+      if (q >= nq) x[q] = __builtin_inff();
+    for (int k = 2; k <= p2; k <<= 1) {
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        if (jj >= FINE_LANES) {
+#pragma unroll
+          for (int bq = 1; bq < QN; bq <<= 1) {
+            if (jj == bq * FINE_LANES) {
+#pragma unroll
+              for (int q = 0; q < QN; ++q) {
+                if ((q & bq) == 0 && q < nr) {
+                  const bool up = ((t + FINE_LANES * q) & k) == 0;
+                  const float a = x[q], b = x[q | bq];
+                  x[q] = up ? fminf(a, b) : fmaxf(a, b);
+                  x[q | bq] = up ? fmaxf(a, b) : fminf(a, b);
+                }
+              }
+            }
+          }
+        } else {
+          const bool lower = (t & jj) == 0;
+#pragma unroll
+          for (int q = 0; q < QN; ++q) {
+            const float o = __shfl_xor(x[q], jj);
+            const bool up = ((t + FINE_LANES * q) & k) == 0;
+            if (q < nr) x[q] = (lower == up) ? fminf(x[q], o) : fmaxf(x[q], o);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < QN; ++q)
+      if (q < nr) zf[t + FINE_LANES * q] = x[q];
+    __builtin_amdgcn_wave_barrier();
   }
   // torch.sort(cat(z, z_fine)) values: merge by rank (ties: coarse first; equal
   // values are interchangeable)

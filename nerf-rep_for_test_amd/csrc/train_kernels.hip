@@ -318,6 +318,7 @@ __global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
   for (int j = lane; j < n_imp; j += 64) {
     const float x = L.zf[j];
     int rank = 0;
+#pragma unroll 8
     for (int k = 0; k < n_imp; ++k) {
       const float y = L.zf[k];
       rank += (y < x) || (y == x && k < j);
@@ -329,6 +330,7 @@ __global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
   // dL/dcdf[k], summed in sample order (deterministic)
   for (int k = lane; k < nb; k += 64) {
     float acc = 0.0f;
+#pragma unroll 4
     for (int j = 0; j < n_imp; ++j) {
       if (L.lo[j] == k) acc += L.gt[j] * L.dc0[j];
       if (L.hi[j] == k) acc += L.gt[j] * L.dc1[j];
@@ -536,7 +538,7 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     if (vec) {   // 16-B loads (4 k per load; the lanes' W_f rows are 1 KiB apart)
       const float4* g4 = reinterpret_cast<const float4*>(g);
       const float4* w4 = reinterpret_cast<const float4*>(w);
-#pragma unroll 4
+#pragma unroll 16
       for (int k = 0; k < 64; ++k) {
         const float4 a = g4[k], b = w4[k];
         acc = __builtin_fmaf(a.x, b.x, acc);
@@ -554,6 +556,7 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
   if (t < kVfFeat) {
     const int a = t >> 8, b = t & 255;
     float acc = 0.0f;
+#pragma unroll 16
     for (int i = 0; i < 128; ++i)
       acc = __builtin_fmaf(Wv[(int64_t)i * 283 + a], GA[(int64_t)i * ldga + b], acc);
     dWf[t] = acc;
@@ -562,6 +565,7 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
   t -= kVfFeat;
   if (t < 256) {
     float acc = 0.0f;
+#pragma unroll 16
     for (int i = 0; i < 128; ++i) acc = __builtin_fmaf(Wv[(int64_t)i * 283 + t], ba[i], acc);
     dbf[t] = acc;
     return;
@@ -613,8 +617,7 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 //   m = m + (1 - b1) (g - m),  v = v b2 + (1 - b2) g g,
 //   p = p - lr / (1 - b1^t) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)),  t = step + 1.
 // lr and the step count live on the device (a HIP graph replays the launch);
-// the last workgroup to finish writes step = t (every workgroup read the old
-// count first).
+// adam_advance_kernel then writes step = t.
 constexpr int kAdamMax = 64;
 constexpr int kAdamPer = 4;                 // elements per thread, loaded together
 constexpr int kAdamBlock = 256 * kAdamPer;  // elements per workgroup (~1 200 workgroups for
@@ -629,8 +632,7 @@ struct AdamBatch {
 // distinct arrays, declared so): one HBM latency per thread instead of one per
 // element, which a loop with a store between dependent loads would expose.
 __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const float* __restrict__ lr,
-                                                   float* __restrict__ step,
-                                                   unsigned* __restrict__ done, double beta1,
+                                                   const float* __restrict__ step, double beta1,
                                                    double beta2, float eps, float clip) {
   const int blk = (int)blockIdx.x;
   int k = 0;
@@ -674,20 +676,17 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const floa
       P[i] = p0[r] + (-step_size) * (m / denom);          // addcdiv_
     }
   }
-  __syncthreads();   // this workgroup's reads of *step are done
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(done, 1u) == gridDim.x - 1) {
-      *step = t;
-      *done = 0u;
-    }
-  }
 }
+
+// step = t after every workgroup of the step has read the old count: the next
+// launch on the stream (a device-wide fence + finish counter per workgroup, as
+// round 3 had it, cost ~30 us: on gfx950 the release writes the XCD's L2 back)
+__global__ void adam_advance_kernel(float* __restrict__ step) { *step = *step + 1.0f; }
 
 extern "C" int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float* step,
                               unsigned* done, double beta1, double beta2, float eps, float clip,
                               nerf_stream_t stream) {
-  NERF_REQUIRE(tensors && lr && step && done && n >= 1 && n <= kAdamMax,
+  NERF_REQUIRE(tensors && lr && step && n >= 1 && n <= kAdamMax,
                "nerf_adam_step: bad arguments");
   AdamBatch b;
   int blocks = 0;
@@ -701,8 +700,10 @@ extern "C" int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float*
   }
   b.nt = n;
   if (blocks == 0) return 0;
+  (void)done;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), b, lr,
-                     step, done, beta1, beta2, eps, clip);
+                     step, beta1, beta2, eps, clip);
+  hipLaunchKernelGGL(adam_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), step);
   return check_launch("adam_kernel");
 }
 

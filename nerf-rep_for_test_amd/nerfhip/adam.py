@@ -50,7 +50,6 @@ class HipAdam(torch.optim.Adam):
             raise ValueError("HipAdam: clip must be None (no clipping) or >= 0")
         self.clip = -1.0 if clip is None else float(clip)   # < 0 tells the kernel: none
         self._count = torch.zeros(1, device=dev, dtype=torch.float32)   # shared step count
-        self._done = torch.zeros(1, device=dev, dtype=torch.int32)     # finished workgroups
         self._key = None
         self._arr = None
 
@@ -104,6 +103,6 @@ class HipAdam(torch.optim.Adam):
             self._key = key
         b1, b2 = g["betas"]
         call("nerf_adam_step", ctypes.addressof(self._arr), len(rows), lr.data_ptr(),
-             self._count.data_ptr(), self._done.data_ptr(), float(b1), float(b2),
+             self._count.data_ptr(), None, float(b1), float(b2),
              float(g["eps"]), self.clip, _lib.stream_of(self._count.device))
         return None

@@ -527,7 +527,8 @@ class _WgradDesc(ctypes.Structure):
                 ("amax_b", ctypes.c_void_p), ("part", ctypes.c_void_p),
                 ("ldpart", ctypes.c_int64), ("bias_part", ctypes.c_void_p),
                 ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int),
-                ("amax_a2", ctypes.c_void_p), ("amax_b2", ctypes.c_void_p)]
+                ("amax_a2", ctypes.c_void_p), ("amax_b2", ctypes.c_void_p),
+                ("ldo", ctypes.c_int64)]
 
 
 _NCU = {}
@@ -591,12 +592,16 @@ class WgradBatch:
         self.device = device
         self.req = []
 
-    def add(self, A, B, amax_a=None, amax_b=None, with_bias=False):
+    def add(self, A, B, amax_a=None, amax_b=None, with_bias=False, width=None, into=None):
+        """width: the result has `width` columns, B's rows the first of them;
+        into = (slot, c0): B's rows are columns c0 .. of slot's result (the
+        same A; no result of its own). One contiguous gradient from operands in
+        two buffers (the skip layer's [encoding | h4])."""
         if amax_a is None:
             amax_a = _absmax(A)
         if amax_b is None:
             amax_b = _absmax(B)
-        self.req.append((A, B, amax_a, amax_b, with_bias))
+        self.req.append((A, B, amax_a, amax_b, with_bias, width, into))
         return len(self.req) - 1
 
     def results(self):
@@ -610,25 +615,45 @@ class WgradBatch:
                   for A, B, *_ in req))
         if not ok:
             one = lambda m: torch.maximum(*m) if isinstance(m, tuple) else m   # noqa: E731
-            return [_wgrad(A, B, one(aa), one(ab), wb) for A, B, aa, ab, wb in req]
+            res = [_wgrad(A, B, one(aa), one(ab), wb) for A, B, aa, ab, wb, _, _ in req]
+            for k, (A, B, _, _, wb, width, into) in enumerate(req):
+                if into is not None:   # the column blocks joined on the host
+                    s, c0 = into
+                    tgt = res[s][0] if isinstance(res[s], tuple) else res[s]
+                    blk = res[k][0] if isinstance(res[k], tuple) else res[k]
+                    tgt[:, c0:c0 + B.shape[0]] = blk
+                    res[k] = None
+                elif width is not None and width != B.shape[0]:
+                    dw = res[k][0] if isinstance(res[k], tuple) else res[k]
+                    full = torch.zeros((A.shape[0], width), device=dw.device, dtype=dw.dtype)
+                    full[:, :B.shape[0]] = dw
+                    res[k] = (full, res[k][1]) if isinstance(res[k], tuple) else full
+            return res
         zs = wgrad_tile_chunks([(A.shape[0], B.shape[0]) for A, B, *_ in req], P, _n_cu(self.device))
         Z = max(zs)
-        sizes = [A.shape[0] * B.shape[0] for A, B, *_ in req]
-        bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb in req]
-        ld, ldb = sum(sizes), max(1, sum(bsizes))
+        # output regions: [M][width] per request that owns one; joined requests
+        # write their column block of the owner's region
+        region, ld = {}, 0
+        for k, (A, B, _, _, _, width, into) in enumerate(req):
+            if into is None:
+                region[k] = (ld, width or B.shape[0])
+                ld += A.shape[0] * (width or B.shape[0])
+        bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb, _, _ in req]
+        ldb = max(1, sum(bsizes))
         part = torch.empty((Z, ld), device=self.device, dtype=torch.float32)
         bpart = torch.empty((Z, ldb), device=self.device, dtype=torch.float32)
         descs = (_WgradDesc * len(req))()
-        off = boff = 0
+        boff = 0
         def two(m):   # a scale given as (tensor, tensor): the kernel takes their max
             return (m[0].data_ptr(), m[1].data_ptr()) if isinstance(m, tuple) else (m.data_ptr(), None)
-        for k, (A, B, aa, ab, wb) in enumerate(req):
+        for k, (A, B, aa, ab, wb, width, into) in enumerate(req):
             (a1, a2), (b1, b2) = two(aa), two(ab)
+            off, wdt = region[into[0]] if into is not None else region[k]
+            off += into[1] if into is not None else 0
             descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
                                   a1, b1, part.data_ptr() + 4 * off, ld,
                                   bpart.data_ptr() + 4 * boff if wb else None, ldb,
-                                  A.shape[0], B.shape[0], a2, b2)
-            off += sizes[k]
+                                  A.shape[0], B.shape[0], a2, b2, wdt)
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
         zarr = (ctypes.c_int * len(zs))(*zs)
@@ -638,10 +663,13 @@ class WgradBatch:
         bflat = torch.empty((ldb,), device=self.device, dtype=torch.float32)
         if boff:
             call("nerf_sum_partials", ptr(bpart), Z, ldb, ptr(bflat), st)
-        out, off, boff = [], 0, 0
-        for k, (A, B, _, _, wb) in enumerate(req):
-            dw = flat[off:off + sizes[k]].view(A.shape[0], B.shape[0])
-            off += sizes[k]
+        out, boff = [], 0
+        for k, (A, B, _, _, wb, _, into) in enumerate(req):
+            if into is not None:
+                out.append(None)
+                continue
+            off, wdt = region[k]
+            dw = flat[off:off + A.shape[0] * wdt].view(A.shape[0], wdt)
             if wb:
                 out.append((dw, bflat[boff:boff + bsizes[k]]))
                 boff += bsizes[k]
@@ -874,14 +902,18 @@ class NerfMLPFn(torch.autograd.Function):
             post[wb.add(d_sig, H[7], dmax[12:13], amax[7:8], with_bias=True)] = (
                 "alpha_linear.weight", "alpha_linear.bias", None)
         for i in range(7, -1, -1):
-            inp = E if i == 5 else (E[0:64] if i == 0 else H[i - 1])
-            in_max = ((amax[9:10], amax[4:5]) if i == 5 else
-                      amax[9:10] if i == 0 else amax[i - 1:i])
-            fix = ((lambda g: g[:, :63]) if i == 0 else
-                   (lambda g: torch.cat([g[:, :63], g[:, 64:320]], 1)) if i == 5 else None)
-            post[wb.add(D[i], inp, dmax[i:i + 1], in_max, with_bias=True)] = (
-                f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", fix)
+            # layer 0 reads the 63 encoding rows; the skip layer's [63 encoding
+            # rows | h4] are two column blocks of one contiguous [256, 319] result
+            # (each with its own scale), so no gradient needs a gather afterwards
+            inp, in_max = (E[0:63], amax[9:10]) if i in (0, 5) else (H[i - 1], amax[i - 1:i])
+            s = wb.add(D[i], inp, dmax[i:i + 1], in_max, with_bias=True,
+                       width=319 if i == 5 else None)
+            post[s] = (f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", None)
+            if i == 5:
+                post[wb.add(D[5], H[4], dmax[5:6], amax[4:5], into=(s, 63))] = None
         for slot, res in enumerate(wb.results()):
+            if post[slot] is None:   # a column block joined into another slot's result
+                continue
             wname, bname, fix = post[slot]
             gw, gb = (res if bname else (res, None))
             grads[wname] = fix(gw) if fix is not None else gw

@@ -219,14 +219,21 @@ def test_sample_fine_given_reference_weights(dev, name):
     assert np.mean(err < 1e-5) >= 0.97
 
 
-@pytest.mark.parametrize("S,NI", [(64, 128), (3, 1), (5, 7), (33, 64), (100, 200), (130, 256)])
-def test_sample_fine_training_u(dev, S, NI):
-    """Training-mode u (unsorted uniform draws, VR:247-249), ragged sizes."""
-    rng = np.random.default_rng(3 + S + NI)
+@pytest.mark.parametrize("S,NI,ties", [(64, 128, False), (3, 1, False), (5, 7, False),
+                                        (33, 64, False), (100, 200, False), (130, 256, False),
+                                        (64, 128, True), (17, 40, True)])
+def test_sample_fine_training_u(dev, S, NI, ties):
+    """Training-mode u (unsorted uniform draws, VR:247-249), ragged sizes; ties:
+    u on a coarse grid (repeated fine depths) and rays with all-zero weights
+    (every bin clamped), so the in-register sort meets equal keys."""
+    rng = np.random.default_rng(3 + S + NI + ties)
     n = 300
     zc = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
     wc = (rng.random((n, S)) ** 4).astype(np.float32)
     u = rng.random((n, NI)).astype(np.float32)
+    if ties:
+        u = (np.floor(u * 8) / 8).astype(np.float32)
+        wc[::7] = 0.0
     zall = torch.empty((n, S + NI), device=dev)
     from nerfhip._lib import call, ptr, stream_of
     zc_d, wc_d, u_d = _t(zc, dev), _t(wc, dev), _t(u, dev)

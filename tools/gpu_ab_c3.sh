@@ -1,24 +1,25 @@
 #!/bin/bash
-# training-kernel A/B on one box: tests of the current library, then the
-# kernel bench and the C3 step for lib/libnerfhip_old.so and the current build
+# A/B of variant libraries (NERFHIP_LIB=lib/libnerfhip_<v>.so, VARIANTS="v1 v2")
+# against the tree's library on the C3 step: bench.py --config c3 (graph),
+# interleaved REPS times, then one rocprofv3 kernel-stats pass per library.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abc3}
 mkdir -p "$OUT"
-step() {
-  local name=$1 t=$2; shift 2
-  echo "== $name ($(date +%T))"
-  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
-  local rc=$?
-  echo "== $name rc=$rc"; tail -n ${TAILN:-6} "$OUT/$name.log" | cut -c1-400
-  [ $rc -eq 0 ] || exit $rc
-}
-step tests 600 python -u -m pytest tests/test_gpu_train_mlp.py tests/test_gpu_train.py -m gpu -q -x --timeout 120 --timeout-method thread ${PYTEST_K:-}
-for v in old new a; do
-  if [ $v = old ]; then export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_old.so; else unset NERFHIP_LIB; fi
-  [ $v = a ] && export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_old.so
-  step kbench_$v 300 python tools/train_kernels_bench.py
-  step c3_$v 300 python bench.py --config c3 --steps 30 --warmup 10 --train-launch eager
+VARIANTS=${VARIANTS:-}
+for rep in $(seq 1 ${REPS:-2}); do
+  for v in base $VARIANTS; do
+    if [ $v = base ]; then unset NERFHIP_LIB; else export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_$v.so; fi
+    timeout -k 10 300 python bench.py --config c3 --steps 30 --warmup 10 --train-launch graph > "$OUT/c3_${v}_$rep.log" 2>&1 || exit $?
+    python -c "import json; d=json.loads(open('$OUT/c3_${v}_$rep.log').read().strip().splitlines()[-1]); print('$v rep $rep c3 ms/step', round(d['ms_per_step'],3))"
+  done
 done
-echo "== done"
+if [ "${PROF:-1}" = 1 ]; then
+  for v in base $VARIANTS; do
+    if [ $v = base ]; then unset NERFHIP_LIB; else export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_$v.so; fi
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$v" -o k \
+      -- python bench.py --config c3 --steps 10 --warmup 3 --train-launch eager > "$OUT/prof_$v.log" 2>&1 || exit $?
+  done
+fi
+echo done
