@@ -112,8 +112,9 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
 /* Backward of _sample_fine with training-mode u (VR:239-268) + the merge
  * torch.sort(cat(z, z_fine)) (VR:181-184) whose forward is nerf_sample_fine:
  * d_weights [n][S] (rows 0 and S-1 zero) from g_zall [n][S + n_imp]. z [n][S],
- * weights [n][S], u [n][n_imp] as given to the forward. S <= 130,
- * n_imp <= 256. */
+ * weights [n][S], u [n][n_imp] as given to the forward; z_all [n][S + n_imp]
+ * the forward's output (nullable: each fine sample's place in the merged row is
+ * then counted instead of searched). S <= 130, n_imp <= 256. */
 /* nerf_adam_step: one Adam step (torch.optim.Adam with weight_decay 0, no
  *   amsgrad; trainers/trainer.py's optimizer) over n <= 64 parameter tensors in
  *   ONE launch, each gradient first clamped in place to [-clip, clip]
@@ -155,7 +156,7 @@ int nerf_mse_pair_backward(const float* a, const float* b, const float* target, 
                            const float* g0, const float* g1, const float* g2, float* da,
                            float* db, nerf_stream_t stream);
 int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
-                        const float* g_zall, int64_t n, int S, int n_imp,
+                        const float* g_zall, const float* z_all, int64_t n, int S, int n_imp,
                         float* d_weights, nerf_stream_t stream);
 
 /* ERT sample compaction (BASELINE configs[3]): nerf_mlp_forward_x3 over the

@@ -1912,7 +1912,8 @@ struct X3HeadGather {
 // block derives the scale exponent from it (and the head blocks are gathered),
 // then a one-thread-per-matrix launch writes the exponent into sw and resets
 // the amax slot for the next packing.
-constexpr int kPackSlabs = 16;   // blocks per matrix
+constexpr int kPackSlabs = 64;   // blocks per matrix (a few loads per thread: the
+                                 // launches are chains of dependent map -> source loads)
 
 __global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __restrict__ descs) {
   const X3PackDesc d = descs[blockIdx.x];
@@ -1923,14 +1924,25 @@ __global__ __launch_bounds__(256) void x3_pack_amax_kernel(const X3PackDesc* __r
   // the max is order-free: walk the source along its contiguous index (a
   // transposed pack reads W column by column otherwise: one line per element)
   const bool by_row = d.ldc > d.ldr;
-  for (int idx = i0 + (int)threadIdx.x; idx < i1; idx += 256) {
-    const int a = by_row ? idx % d.M : idx / d.K, c = by_row ? idx / d.M : idx % d.K;
-    const int ri = d.rowmap[a], ck = d.colmap[c];
-    if (ri >= 0 && ck >= 0) mx = fmaxf(mx, fabsf(d.src[ri * d.ldr + ck * d.ldc]));
+  for (int base = i0 + (int)threadIdx.x; base < i1; base += 4 * 256) {
+    int ri[4], ck[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // every map load of the batch, then every source load
+      const int idx = base + 256 * u;
+      const int a = by_row ? idx % d.M : idx / d.K, c = by_row ? idx / d.M : idx % d.K;
+      ri[u] = idx < i1 ? d.rowmap[a] : -1;
+      ck[u] = idx < i1 ? d.colmap[c] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (ri[u] >= 0 && ck[u] >= 0) mx = fmaxf(mx, fabsf(d.src[ri[u] * d.ldr + ck[u] * d.ldc]));
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0)   // values >= 0: the float bits order like the floats
-    atomicMax(d.amax, __float_as_uint(mx));
+  __shared__ float wmax[4];   // one device atomic per block (64 per matrix word)
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0)   // values >= 0: the float bits order like the floats
+    atomicMax(d.amax, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
 }
 
 __device__ __forceinline__ int pack_exponent(float amax) {

@@ -914,12 +914,16 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
 // The same gradient taken on to the depths of the samples p = ray * S + step
 // at o + d * z (VR:165; rays constant): dz[p] = sum_c dx_c * d_c, as torch's
 // autograd of rays_o + rays_d * z sums it (mul, then the 3-term reduction).
+// LC > 0: L == LC at compile time (every band's loads unrolled and in flight
+// together; the runtime loop exposes one load latency per band)
+template <int LC>
 __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
     const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
-    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P, int L,
+    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P, int Lr,
     float* __restrict__ dz) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
+  const int L = LC > 0 ? LC : Lr;
   auto de = [&](int row) {
     float v = d_enc[row * ldd + p];
     if (d_enc2) v = v + d_enc2[row * ldd + p];
@@ -930,6 +934,7 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     float g = de(c);
+#pragma unroll
     for (int f = 0; f < L; ++f) {
       const float k = (float)(1 << f);
       const float sn = enc[(3 + 6 * f + c) * ldd + p];
@@ -1174,8 +1179,14 @@ int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int
   NERF_REQUIRE(P >= 0 && S >= 1 && P % S == 0 && ldd >= P && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm_backward_dz: bad size");
   if (P == 0) return 0;
-  hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
-                     as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P, n_freq, dz);
+  if (n_freq == 10)   // the xyz encoding (L = 10)
+    hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel<10>, dim3((unsigned)cdiv(P, 256)),
+                       dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P,
+                       n_freq, dz);
+  else
+    hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel<0>, dim3((unsigned)cdiv(P, 256)),
+                       dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P,
+                       n_freq, dz);
   return check_launch("freq_encode_fm_backward_dz_kernel");
 }
 

@@ -210,6 +210,7 @@ constexpr int PDF_WAVES = 4;
 constexpr int PDF_MAX_S = 130;
 constexpr int PDF_MAX_IMP = 256;
 constexpr int PDF_ROW = PDF_MAX_S + 2;
+constexpr int PDF_MAX_ALL = PDF_MAX_S + PDF_MAX_IMP;
 
 struct PdfLds {
   float zc[PDF_ROW];
@@ -217,10 +218,9 @@ struct PdfLds {
   float cdf[PDF_ROW];
   float bins[PDF_ROW];
   float zf[PDF_MAX_IMP];      // fine samples (u order)
-  float gt[PDF_MAX_IMP];      // dL/dt_j
-  float dc0[PDF_MAX_IMP];     // dt_j/dc[below_j]
-  float dc1[PDF_MAX_IMP];     // dt_j/dc[above_j]
-  short lo[PDF_MAX_IMP], hi[PDF_MAX_IMP];
+  float4 c01[PDF_MAX_IMP];    // per fine sample: dL/dcdf[below], dL/dcdf[above], below | above << 16
+  float gz[PDF_MAX_ALL];      // the ray's row of dL/dz_all
+  float za[PDF_MAX_ALL];      // the ray's merged depths (z_all), when given
   float gcdf[PDF_ROW];
   float gpdf[PDF_ROW];
 };
@@ -263,23 +263,41 @@ __device__ __forceinline__ int ub(const float* a, int n, float x) {   // # a[i] 
 }
 
 // d_w [n, S] = dL/dweights of the coarse pass given g_zall [n, S + n_imp]
-// (dL/d z_all). z [n, S] coarse depths (per-ray rows), weights [n, S], u [n, n_imp].
+// (dL/d z_all). z [n, S] coarse depths (per-ray rows), weights [n, S], u [n, n_imp],
+// z_all [n, S + n_imp] the forward's merged rows (nullable).
+// A fine sample's place in the merged row is its rank among the fine samples
+// (ties in u order) + the coarse depths <= it (torch.sort of cat(z, z_f), coarse
+// first on ties); with z_all given it is found by one search of the row, the
+// rank count over all fine samples only for a sample whose value occurs twice.
+// Every row of the ray (depths, its dL/dz_all row, z_all) is staged into LDS at
+// the start, so no global load waits inside the per-sample steps.
 __global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
     const float* __restrict__ z, const float* __restrict__ weights, const float* __restrict__ u,
-    const float* __restrict__ g_zall, int64_t n, int S, int n_imp, float* __restrict__ d_w) {
+    const float* __restrict__ g_zall, const float* __restrict__ z_all, int64_t n, int S,
+    int n_imp, float* __restrict__ d_w) {
   __shared__ PdfLds sm[PDF_WAVES];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t ray = (int64_t)blockIdx.x * PDF_WAVES + wave;
   if (ray >= n) return;   // wave-uniform; no block barriers below
   PdfLds& L = sm[wave];
+  const int nall = S + n_imp;
   const float* zr = z + ray * S;
   const float* wr = weights + ray * S;
   const float* ur = u + ray * n_imp;
-  const float* gz = g_zall + ray * (int64_t)(S + n_imp);
+  const float* gz = g_zall + ray * (int64_t)nall;
   const int nb = S - 1, nw = S - 2;
   for (int s = lane; s < S; s += 64) L.zc[s] = zr[s];
   for (int s = lane; s < nw; s += 64) L.wv[s] = wr[s + 1] + 1e-5f;
+  for (int s = lane; s < nall; s += 64) L.gz[s] = gz[s];
+  if (z_all)
+    for (int s = lane; s < nall; s += 64) L.za[s] = z_all[ray * (int64_t)nall + s];
+  float uj[PDF_MAX_IMP / 64];
+#pragma unroll
+  for (int q = 0; q < PDF_MAX_IMP / 64; ++q) {
+    const int j = lane + 64 * q;
+    uj[q] = j < n_imp ? ur[j] : 0.0f;
+  }
   __builtin_amdgcn_wave_barrier();
   for (int s = lane; s < nb; s += 64) L.bins[s] = 0.5f * (L.zc[s + 1] + L.zc[s]);
   const float tot = wave_tsum_last_pdf(L.wv, nw, lane);
@@ -294,46 +312,63 @@ __global__ __launch_bounds__(64 * PDF_WAVES) void sample_pdf_bwd_kernel(
   }
   __builtin_amdgcn_wave_barrier();
   // recompute each fine sample and the derivatives of its t
-  for (int j = lane; j < n_imp; j += 64) {
-    const float uj = ur[j];
-    const int inds = ub(L.cdf, nb, uj);
-    const int below = inds - 1 > 0 ? inds - 1 : 0;
-    const int above = inds < nb - 1 ? inds : nb - 1;
-    const float c0 = L.cdf[below], c1 = L.cdf[above];
-    const float b0 = L.bins[below], b1 = L.bins[above];
-    const float D = c1 - c0;
-    const bool clamped = D < 1e-5f;
-    const float den = clamped ? 1.0f : D;
-    const float t = (uj - c0) / den;
-    L.zf[j] = b0 + t * (b1 - b0);
-    L.lo[j] = (short)below;
-    L.hi[j] = (short)above;
-    L.dc0[j] = clamped ? -1.0f : (t - 1.0f) / den;
-    L.dc1[j] = clamped ? 0.0f : -t / den;
-    L.gt[j] = b1 - b0;   // times dL/dz_f, below
-  }
-  __builtin_amdgcn_wave_barrier();
-  // position of fine sample j in the merged row: its rank among the fine samples
-  // (ties in u order) + the coarse depths <= it (torch.sort of cat(z, z_f))
-  for (int j = lane; j < n_imp; j += 64) {
-    const float x = L.zf[j];
-    int rank = 0;
-#pragma unroll 8
-    for (int k = 0; k < n_imp; ++k) {
-      const float y = L.zf[k];
-      rank += (y < x) || (y == x && k < j);
+  float dc0[PDF_MAX_IMP / 64], dc1[PDF_MAX_IMP / 64], tf[PDF_MAX_IMP / 64];
+  int lohi[PDF_MAX_IMP / 64];
+#pragma unroll
+  for (int q = 0; q < PDF_MAX_IMP / 64; ++q) {
+    const int j = lane + 64 * q;
+    if (j < n_imp) {
+      const int inds = ub(L.cdf, nb, uj[q]);
+      const int below = inds - 1 > 0 ? inds - 1 : 0;
+      const int above = inds < nb - 1 ? inds : nb - 1;
+      const float c0 = L.cdf[below], c1 = L.cdf[above];
+      const float b0 = L.bins[below], b1 = L.bins[above];
+      const float D = c1 - c0;
+      const bool clamped = D < 1e-5f;
+      const float den = clamped ? 1.0f : D;
+      const float t = (uj[q] - c0) / den;
+      L.zf[j] = b0 + t * (b1 - b0);
+      lohi[q] = below | (above << 16);
+      dc0[q] = clamped ? -1.0f : (t - 1.0f) / den;
+      dc1[q] = clamped ? 0.0f : -t / den;
+      tf[q] = b1 - b0;   // times dL/dz_f, below
     }
-    const int pos = rank + ub(L.zc, S, x);
-    L.gt[j] = L.gt[j] * gz[pos];
   }
   __builtin_amdgcn_wave_barrier();
-  // dL/dcdf[k], summed in sample order (deterministic)
+  // position of fine sample j in the merged row, its dL/dt, and its two cdf terms
+#pragma unroll
+  for (int q = 0; q < PDF_MAX_IMP / 64; ++q) {
+    const int j = lane + 64 * q;
+    if (j < n_imp) {
+      const float x = L.zf[j];
+      int pos = -1;
+      if (z_all) {   // unique value: the last entry <= x is this sample
+        const int up = ub(L.za, nall, x);
+        if (up >= 1 && L.za[up - 1] == x && (up < 2 || L.za[up - 2] != x)) pos = up - 1;
+      }
+      if (pos < 0) {
+        int rank = 0;
+#pragma unroll 8
+        for (int k = 0; k < n_imp; ++k) {
+          const float y = L.zf[k];
+          rank += (y < x) || (y == x && k < j);
+        }
+        pos = rank + ub(L.zc, S, x);
+      }
+      const float gt = tf[q] * L.gz[pos];
+      L.c01[j] = make_float4(gt * dc0[q], gt * dc1[q], __int_as_float(lohi[q]), 0.0f);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // dL/dcdf[k], summed in sample order (deterministic): one 16-B broadcast read per sample
   for (int k = lane; k < nb; k += 64) {
     float acc = 0.0f;
-#pragma unroll 4
+#pragma unroll 8
     for (int j = 0; j < n_imp; ++j) {
-      if (L.lo[j] == k) acc += L.gt[j] * L.dc0[j];
-      if (L.hi[j] == k) acc += L.gt[j] * L.dc1[j];
+      const float4 c = L.c01[j];
+      const int lh = __float_as_int(c.z);
+      if ((lh & 0xffff) == k) acc += c.x;
+      if ((lh >> 16) == k) acc += c.y;
     }
     L.gcdf[k] = acc;
   }
@@ -471,15 +506,15 @@ int nerf_composite_train_bwd(const float* raw, const float* z, const float* rays
 }
 
 int nerf_sample_pdf_bwd(const float* z, const float* weights, const float* u,
-                        const float* g_zall, int64_t n, int S, int n_imp, float* d_weights,
-                        nerf_stream_t stream) {
+                        const float* g_zall, const float* z_all, int64_t n, int S, int n_imp,
+                        float* d_weights, nerf_stream_t stream) {
   NERF_REQUIRE(z && weights && u && g_zall && d_weights, "nerf_sample_pdf_bwd: null pointer");
   NERF_REQUIRE(n >= 0 && S >= 3 && S <= PDF_MAX_S && n_imp >= 1 && n_imp <= PDF_MAX_IMP,
                "nerf_sample_pdf_bwd: bad size");
   if (n == 0) return 0;
   hipLaunchKernelGGL(sample_pdf_bwd_kernel, dim3((unsigned)cdiv(n, PDF_WAVES)),
-                     dim3(64 * PDF_WAVES), 0, as_stream(stream), z, weights, u, g_zall, n, S,
-                     n_imp, d_weights);
+                     dim3(64 * PDF_WAVES), 0, as_stream(stream), z, weights, u, g_zall, z_all, n,
+                     S, n_imp, d_weights);
   return check_launch("sample_pdf_bwd_kernel");
 }
 

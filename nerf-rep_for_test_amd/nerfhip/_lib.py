@@ -49,7 +49,7 @@ SIGNATURES = {
     "nerf_views_feature_grads": (_I, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _S]),
     "nerf_mse_pair": (_I, [_P, _P, _P, _I64, _P, _S]),
     "nerf_mse_pair_backward": (_I, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _S]),
-    "nerf_sample_pdf_bwd": (_I, [_P, _P, _P, _P, _I64, _I, _I, _P, _S]),
+    "nerf_sample_pdf_bwd": (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _S]),
     "nerf_freq_encode_fm": (_I, [_P, _I64, _I64, _I, _P, _I64, _P, _S]),
     "nerf_freq_encode_fm_backward": (_I, [_P, _I64, _P, _I64, _I64, _I, _P, _S]),
     "nerf_raw_absmax": (_I, [_P, _I64, _P, _S]),

@@ -70,18 +70,19 @@ class SampleFineFn(torch.autograd.Function):
         zall = torch.empty((n, S + NI), device=z.device, dtype=torch.float32)
         call("nerf_sample_fine", ptr(z_c), S, ptr(w_c), ptr(u_c), NI, n, S, NI, ptr(zall),
              _lib.stream_of(z.device))
-        ctx.save_for_backward(w_c, z_c, u_c)
+        ctx.save_for_backward(w_c, z_c, u_c, zall)
         ctx.set_materialize_grads(False)
         return zall
 
     @staticmethod
     def backward(ctx, g_zall):
-        w, z, u = ctx.saved_tensors
+        w, z, u, zall = ctx.saved_tensors
         if g_zall is None or not ctx.needs_input_grad[0]:
             return None, None, None
         n, S = z.shape
         d_w = torch.empty_like(w)
-        call("nerf_sample_pdf_bwd", ptr(z), ptr(w), ptr(u), ptr(g_zall.contiguous()), n, S,
+        g = g_zall.contiguous()
+        call("nerf_sample_pdf_bwd", ptr(z), ptr(w), ptr(u), ptr(g), ptr(zall), n, S,
              u.shape[1], ptr(d_w), _lib.stream_of(z.device))
         return d_w, None, None
 

@@ -169,3 +169,35 @@ def test_x3_clock_twin_computes_the_same(dev):
     assert used.sum() == min(-(-n * S // 128), torch.cuda.get_device_properties(dev).multi_processor_count)
     ghz = (c[used, 1] - c[used, 0]) / (c[used, 3] - c[used, 2]) * 0.1
     assert 0.5 < np.median(ghz) < 3.0, np.median(ghz)
+
+
+@pytest.mark.parametrize("S,NI,ties", [(64, 128, False), (64, 128, True), (17, 40, True),
+                                        (130, 256, False)])
+def test_sample_pdf_bwd_search_equals_count(dev, S, NI, ties):
+    """nerf_sample_pdf_bwd with the forward's z_all (each fine sample's place
+    found by one search of the merged row, the rank count only for a repeated
+    value) is bit-equal to the count over all fine samples (z_all NULL); ties:
+    u on a coarse grid and all-zero weight rows, so values repeat (fine-fine and
+    fine-coarse)."""
+    from nerfhip._lib import call, ptr, stream_of
+    rng = np.random.default_rng(7 + S + NI + ties)
+    n = 300
+    z = np.sort(rng.uniform(2, 6, (n, S)), 1).astype(np.float32)
+    w = (rng.random((n, S)) ** 3).astype(np.float32)
+    u = rng.random((n, NI)).astype(np.float32)
+    if ties:
+        u = (np.floor(u * 8) / 8).astype(np.float32)
+        w[::5] = 0.0
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    zt, wt, ut = t(z), t(w), t(u)
+    zall = torch.empty((n, S + NI), device=dev)
+    call("nerf_sample_fine", ptr(zt), S, ptr(wt), ptr(ut), NI, n, S, NI, ptr(zall), stream_of(dev))
+    g = torch.randn(zall.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+    out = []
+    for za in (zall, None):
+        d = torch.empty_like(wt)
+        call("nerf_sample_pdf_bwd", ptr(zt), ptr(wt), ptr(ut), ptr(g), ptr(za), n, S, NI, ptr(d),
+             stream_of(dev))
+        out.append(d.cpu())
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
