@@ -55,7 +55,7 @@ CKPT_DIR = os.path.join(REPO, "checkpoints", "lego")
 TOL = 1e-5
 DPSNR = 0.01
 FRAC = 0.999        # fine rgb within 1e-5
-FRAC_ALL = 0.995    # every fine map within tolerance or 4x the reference's own spread
+FRAC_ALL = 0.999    # every fine map within tolerance or 4x the reference's own spread (measured >= 0.99944)
 
 
 @pytest.fixture(scope="module")
