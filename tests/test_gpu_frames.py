@@ -25,7 +25,7 @@ held to:
   differ from the reference's (a searchsorted / denom-clamp flip of the
   ill-conditioned fine sampling, VR:239-268; tests/goldlib.py attribute_tail)
   or, with ERT, its 2048-ray chunk holds such a ray. tail_unexplained == 0;
-* >= 99.9 % of the pixels within tolerance on fine rgb, >= 99.5 % within
+* >= 99.9 % of the pixels within tolerance on fine rgb, >= 99.9 % within
   tolerance or 4x the reference's own spread on every fine map (the rest are
   the attributed sampling flips), and
   PSNR(HIP vs reference) >= 60 dB;
