@@ -1649,11 +1649,14 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 // splits the fragments it reads (FP32 -> FP16 hi/lo) in registers. A K step
 // (32 samples) is two granules of 32 KiB, A_k (256 rows of A) then B_k, and
 // the granules stream through a 5-slot ring (160 KiB, all of the CU's LDS):
-// while step k is multiplied, B_{k+1}, A_{k+1} and A_{k+2} are landing. A
-// wave's 8 LDS-DMA pieces of a step (4 of B_{k+1}, then 4 of A_{k+2}) are
-// issued one per B tile of its MFMA loop, so their issue cost overlaps the
-// MFMAs (issued all at once after the step's barrier, every wave of the CU
-// stalled on them together with the MFMA pipes idle).
+// while step k is multiplied, A_{k+1}, B_{k+1}, A_{k+2} and B_{k+2} are
+// landing -- B_{k+2} in A_k's slot, freed by a mid-step barrier once every wave
+// holds its A_k fragments (before it, a B granule was issued one step ahead
+// and had about one step to land). A wave's 8 LDS-DMA pieces of a step (4 of
+// A_{k+2}, then 4 of B_{k+2}) are issued one per B tile of its MFMA loop, so
+// their issue cost overlaps the MFMAs (issued all at once after the step's
+// barrier, every wave of the CU stalled on them together with the MFMA pipes
+// idle).
 // Piece (t, h) of a granule = 16-row tile t, half h: lane l holds row
 // 16t + (l & 15), samples 8 (l >> 4) + 4h .. +3, so the two halves read by
 // lane l are one MFMA fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past
@@ -1729,18 +1732,22 @@ __device__ __forceinline__ void wgrad_dma_body(
     return __builtin_bit_cast(Op, __builtin_shufflevector(r.x, r.y, 0, 1, 2, 3, 4, 5, 6, 7));
   };
 
-  // prologue: granules 0 .. 2 (A_0, B_0, A_1)
-  for (int g = 0; g < 3 && g < ngran; ++g) issue(g);
+  // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1)
+  for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
   for (int k = 0; k < nsteps; ++k) {
-    // granules <= 2k+1 landed (this wave's pieces); 2k+2 (4 pieces) may stay in flight
-    if (2 * k + 2 < ngran) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // granules <= 2k+1 landed (this wave's pieces); 2k+2, 2k+3 (8 pieces) may stay in flight
+    if (k + 1 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // everyone's landed; slots of step k-1 are free
+    __builtin_amdgcn_s_barrier();   // everyone's landed; B_{k-1}'s slot is free
     asm volatile("" ::: "memory");
-    const int gb = 2 * k + 3, ga = 2 * k + 4;   // B_{k+1}, A_{k+2}: issued during this step
+    // A_{k+2} into B_{k-1}'s slot from the start of the step; B_{k+2} into A_k's
+    // slot after a mid-step barrier (every wave holds its A_k fragments by then),
+    // so a B granule has 1.5 steps to land instead of one
+    const int ga = 2 * k + 4, gb = 2 * k + 5;
     if (!busy) {   // nothing to multiply: stage this wave's pieces at once
-      issue(gb);
       issue(ga);
+      __builtin_amdgcn_s_barrier();
+      issue(gb);
       continue;
     }
     const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
@@ -1767,9 +1774,11 @@ __device__ __forceinline__ void wgrad_dma_body(
       if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
       Op b = to_op(cur);
       if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
-      // one LDS-DMA piece per B tile: B_{k+1} pieces 0-3, then A_{k+2} pieces 0-3
-      if constexpr (j < 4) issue_piece(gb, std::integral_constant<int, j>{});
-      else issue_piece(ga, std::integral_constant<int, j - 4>{});
+      // one LDS-DMA piece per B tile: A_{k+2} pieces 0-3, the mid-step barrier,
+      // then B_{k+2} pieces 0-3
+      if constexpr (j == 4) __builtin_amdgcn_s_barrier();
+      if constexpr (j < 4) issue_piece(ga, std::integral_constant<int, j>{});
+      else issue_piece(gb, std::integral_constant<int, j - 4>{});
       split_op(b, sb);
       const half8 bh = op_hi(b), bl = op_lo(b);
 #pragma unroll
