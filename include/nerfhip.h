@@ -298,7 +298,8 @@ int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float* w_head,
  *   d[0] = the gradients of the pre-activations of layers 7 .. 0 (256 rows
  *   each); with_enc also d[10] / d[11] = the xyz encoding's gradient through
  *   layer 5 / layer 0 (64 rows; row 63 is padding). io->dmax[0..8], [10]
- *   (caller-initialised, >= 0) are raised to the outputs' max |.|. d[8] may be
+ *   (caller-initialised, >= 0) are raised to the outputs' max |.|, [11] / [12]
+ *   to max |d rgb| / |d sigma| of d_raw. d[8] may be
  *   NULL: d feature is then not written (dW_feat = W_views,feat^T G, see
  *   NerfX3TrainOut). */
 typedef struct NerfX3BwdIO {

@@ -961,7 +961,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     const X3BwdIO io) {
   __shared__ __attribute__((aligned(16))) float ring[4 * kSliceFloats];
   __shared__ __attribute__((aligned(16))) float hd[kHeadFloats];
-  __shared__ unsigned dmax_lds[11];
+  __shared__ unsigned dmax_lds[13];
   __shared__ __attribute__((aligned(16))) float mask_lds[8 * 128];   // 512 B per wave
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -972,7 +972,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, 72));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
-  if (tid < 11) dmax_lds[tid] = 0u;
+  if (tid < 13) dmax_lds[tid] = 0u;
 
   FragPipe fp;
   fp.ns = kNs;
@@ -990,6 +990,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   // (unwritten) mask words of their tile say, and no max |.| sees them
   float4 dr = io.d_raw[gl];
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  // max |d rgb| and |d sigma| (the heads' wgrad scales, slots 11 / 12): every
+  // lane group holds its samples' d raw, so lane group 0 reports
+  if (g4 == 0) {
+    lds_max_u32(&dmax_lds[11], __float_as_uint(fmaxf(fmaxf(fabsf(dr.x), fabsf(dr.y)), fabsf(dr.z))));
+    lds_max_u32(&dmax_lds[12], __float_as_uint(fabsf(dr.w)));
+  }
   if (io.d_raw_t && g4 == 0 && valid) {   // d raw feature-major: the heads' wgrad operands
     float* t = io.d_raw_t + gs;
     t[0] = dr.w;
@@ -1159,7 +1165,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   __syncthreads();
   float* dm = io.dmax;
   asm volatile("" : "+s"(dm));
-  if (wave == 0 && lane < 11 && lane != 9)
+  if (wave == 0 && lane < 13 && lane != 9)
     atomicMax(reinterpret_cast<unsigned*>(dm) + lane, dmax_lds[lane]);
 }
 

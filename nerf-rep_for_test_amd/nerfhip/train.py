@@ -290,6 +290,7 @@ class NerfTrainer:
             self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0,
                                         fused=self.device.type == "cuda")
         self._graphs = {}
+        self._one = {}
         self._warm = {}
         self.z_base = coarse_depth_table(near, far, self.N_samples, False).to(self.device)
 
@@ -363,8 +364,8 @@ class NerfTrainer:
     def _step_graphed(self, rays_o, rays_d, target, t_rand, u, group):
         key = (rays_o.shape[0], group is not None)
         g = self._graphs.get(key)
-        t_rand, u = self._draws(rays_o.shape[0], t_rand, u)
         if g is None:
+            t_rand, u = self._draws(rays_o.shape[0], t_rand, u)
             if self._warm.get(key, 0) < 2:
                 self._warm[key] = self._warm.get(key, 0) + 1
                 return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
@@ -375,9 +376,16 @@ class NerfTrainer:
             with torch.cuda.graph(graph):
                 out = self._step_eager(*static, group)
             g = self._graphs[key] = (graph, static, out)
+            t_rand = u = None   # already in the static inputs
+            given = (rays_o, rays_d, target, static[3], static[4])
+        else:
+            given = (rays_o, rays_d, target, t_rand, u)
         graph, static, out = g
-        for dst, src in zip(static, (rays_o, rays_d, target, t_rand, u)):
-            dst.copy_(src)
+        for i, (dst, src) in enumerate(zip(static, given)):
+            if src is None:   # the step's draw, straight into the graph's input (t_rand, then u)
+                torch.rand(dst.shape, device=dst.device, out=dst)
+            elif src is not dst:
+                dst.copy_(src)
         graph.replay()
         return out
 
@@ -388,7 +396,11 @@ class NerfTrainer:
             from .train_mlp import prepack
             prepack([self.coarse] + ([self.fine] if self.N_importance > 0 else []))
         losses = self.loss(self.forward(rays_o, rays_d, t_rand, u), target)
-        losses["loss"].backward()
+        loss = losses["loss"]
+        one = self._one.get(loss.device)
+        if one is None:   # d loss / d loss = 1, kept (no fill kernel per step)
+            one = self._one[loss.device] = torch.ones((), device=loss.device, dtype=loss.dtype)
+        loss.backward(one)
         if group is not None:   # parameters without a gradient (e.g. no fine pass) skipped
             allreduce_mean([p.grad for p in self.parameters() if p.grad is not None], group)
         if self.adam != "hip":   # (HipAdam clamps the gradients itself, in place)

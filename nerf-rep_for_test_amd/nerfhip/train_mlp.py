@@ -639,9 +639,11 @@ class WgradBatch:
                 region[k] = (ld, width or B.shape[0])
                 ld += A.shape[0] * (width or B.shape[0])
         bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb, _, _ in req]
-        ldb = max(1, sum(bsizes))
-        part = torch.empty((Z, ld), device=self.device, dtype=torch.float32)
-        bpart = torch.empty((Z, ldb), device=self.device, dtype=torch.float32)
+        ldb = sum(bsizes)
+        # weight and bias partials side by side in one [Z][ld + ldb] array: one
+        # fixed-order sum for both
+        ldt = ld + ldb
+        part = torch.empty((Z, ldt), device=self.device, dtype=torch.float32)
         descs = (_WgradDesc * len(req))()
         boff = 0
         def two(m):   # a scale given as (tensor, tensor): the kernel takes their max
@@ -651,18 +653,16 @@ class WgradBatch:
             off, wdt = region[into[0]] if into is not None else region[k]
             off += into[1] if into is not None else 0
             descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
-                                  a1, b1, part.data_ptr() + 4 * off, ld,
-                                  bpart.data_ptr() + 4 * boff if wb else None, ldb,
+                                  a1, b1, part.data_ptr() + 4 * off, ldt,
+                                  part.data_ptr() + 4 * (ld + boff) if wb else None, ldt,
                                   A.shape[0], B.shape[0], a2, b2, wdt)
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
         zarr = (ctypes.c_int * len(zs))(*zs)
         call("nerf_x3_wgrad_batch_z", ctypes.addressof(descs), len(req), zarr, Z, st)
-        flat = torch.empty((ld,), device=self.device, dtype=torch.float32)
-        call("nerf_sum_partials", ptr(part), Z, ld, ptr(flat), st)
-        bflat = torch.empty((ldb,), device=self.device, dtype=torch.float32)
-        if boff:
-            call("nerf_sum_partials", ptr(bpart), Z, ldb, ptr(bflat), st)
+        total = torch.empty((ldt,), device=self.device, dtype=torch.float32)
+        call("nerf_sum_partials", ptr(part), Z, ldt, ptr(total), st)
+        flat, bflat = total[:ld], total[ld:]
         out, boff = [], 0
         for k, (A, B, _, _, wb, _, into) in enumerate(req):
             if into is not None:
@@ -738,7 +738,8 @@ class NerfMLPFn(torch.autograd.Function):
         # max |.| of every saved activation (the weight-gradient scales): slots
         # 0-7 = h0..h7 and 8 = feature from the layer kernels, 9 = xyz encoding,
         # 10 = view encoding (both from the encoding kernel), 11 = views layer
-        amax = torch.zeros(12, device=dev, dtype=f32)
+        stats = torch.zeros(25, device=dev, dtype=f32)   # amax + the backward's dmax: one fill
+        amax, ctx.dmax_buf = stats[:12], stats[12:]
         pts_c = pts.detach().contiguous()
         fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
         if not fused_f:   # (the fused forward writes the encoding rows itself)
@@ -866,12 +867,17 @@ class NerfMLPFn(torch.autograd.Function):
         wb = WgradBatch(dev)   # every weight gradient below: one batched launch at the end
         post = {}              # slot -> (weight name, bias name or None, column fix-up)
         # max |d| of each product (slots as NerfX3BwdIO.dmax); [11] / [12]: of
-        # d rgb / d sigma (one pass over d_raw)
-        dmax = torch.zeros(13, device=dev, dtype=f32)
+        # d rgb / d sigma
+        # (zeroed with the forward's maxima; a second backward of the same graph
+        # only raises them further: a larger scale, still a valid one)
+        dmax = getattr(ctx, "dmax_buf", None)
+        if dmax is None:
+            dmax = torch.zeros(13, device=dev, dtype=f32)
         d_raw_c = d_raw.detach().to(f32).contiguous()
         if d_raw_c.data_ptr() % 16:
             d_raw_c = d_raw_c.clone()
-        call("nerf_raw_absmax", ptr(d_raw_c), P, ptr(dmax[11:]), _lib.stream_of(dev))
+        if not ctx.fused_backward:   # (the fused backward kernel raises [11] / [12] itself)
+            call("nerf_raw_absmax", ptr(d_raw_c), P, ptr(dmax[11:]), _lib.stream_of(dev))
         # the heads' bias gradients come out of the batched launch too (its row
         # sums), not from separate reductions over P
         rays_S = getattr(ctx, "rays_S", 0)   # RayMLPFn: the gradient goes to z [n, S]
@@ -1066,7 +1072,8 @@ class RayMLPFn(torch.autograd.Function):
         P = n * S
         dev = z.device
         E = _act(320, P, dev)
-        amax = torch.zeros(12, device=dev, dtype=torch.float32)
+        stats = torch.zeros(25, device=dev, dtype=torch.float32)   # amax + the backward's dmax
+        amax, ctx.dmax_buf = stats[:12], stats[12:]
         H = [_act(256, P, dev) if i not in (4, 7) else None for i in range(8)]
         H[4] = E[64:320]                             # h7: V's rows (_forward_fused)
         ctx.fused_backward = FUSED_BACKWARD and P > 0

@@ -332,6 +332,41 @@ def test_x3_wgrad_batch_matches_matmul(dev):
                 assert (gb.double() - rb).abs().max().item() / A.double().abs().sum(1).max().item() < 1e-6
 
 
+def test_x3_wgrad_batch_joined_column_blocks(dev):
+    """WgradBatch column blocks: add(A, B1, width=W) + add(A, B2, into=(slot, c0))
+    give one contiguous [M, W] gradient [A B1^T | A B2^T] (the skip layer's
+    [63 encoding rows | h4], each block with its own scale: nerf_x3_wgrad_batch
+    descriptors with ldo), next to ordinary requests sharing the same partial
+    sum; with P % 32 != 0 the host joins the per-layer results the same way."""
+    from nerfhip.train_mlp import WgradBatch
+    g = torch.Generator(device=dev).manual_seed(9)
+    for P in (4096, 1000):
+        A = torch.randn((256, P + 32), device=dev, generator=g)[:, :P]
+        B1 = torch.randn((63, P + 32), device=dev, generator=g)[:, :P] * 3.0
+        B2 = torch.relu(torch.randn((256, P + 32), device=dev, generator=g))[:, :P] * 0.01
+        C = torch.randn((128, P + 32), device=dev, generator=g)[:, :P]
+        wb = WgradBatch(dev)
+        s0 = wb.add(C, B2, with_bias=True)
+        s1 = wb.add(A, B1, with_bias=True, width=319)
+        s2 = wb.add(A, B2, into=(s1, 63))
+        res = wb.results()
+        assert res[s2] is None
+        got, gb = res[s1]
+        assert got.shape == (256, 319) and got.is_contiguous()
+        ref = torch.cat([A.double() @ B1.double().t(), A.double() @ B2.double().t()], 1)
+        for c0, c1, B in ((0, 63, B1), (63, 319, B2)):   # each block against its own scale
+            scale = (A.double().abs() @ B.double().abs().t()).max().item()
+            assert (got[:, c0:c1].double() - ref[:, c0:c1]).abs().max().item() / scale < 1e-6, P
+        assert (gb.double() - A.double().sum(1)).abs().max().item() / \
+            A.double().abs().sum(1).max().item() < 1e-6
+        other, ob = res[s0]
+        ref0 = C.double() @ B2.double().t()
+        scale0 = (C.double().abs() @ B2.double().abs().t()).max().item()
+        assert (other.double() - ref0).abs().max().item() / scale0 < 1e-6
+        assert (ob.double() - C.double().sum(1)).abs().max().item() / \
+            C.double().abs().sum(1).max().item() < 1e-6
+
+
 def test_x3_stream_packer_matches_host_packing(dev):
     """X3StreamPacker (nerf_x3_pack into the 73-slice stream + the head gather)
     == nerfhip.pack.pack_mlp_x3(fold=False): the stream bit for bit, the head
