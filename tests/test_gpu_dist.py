@@ -1,4 +1,5 @@
-"""The real sharded render path on the GPU: two fresh processes (ranks over
+"""The real sharded render path (and the data-parallel training step) on the
+GPU: two fresh processes (ranks over
 gloo, both on cuda:0) run bench.py's own frame function
 (``bench.make_frame_fn``: C2 row bands + all-gather; C4 2048-ray chunks dealt
 round-robin with the ESS grid's self-updates replayed) and the
@@ -87,3 +88,39 @@ def test_c4_interleaved_chunks_equal_one_pass_frame(ranks, counter):
     assert sum(int(rec[p + "evaluated"]) for rec in ranks) == int(one["one_" + p + "evaluated"])
     # the C4 frame really terminates rays (acc = 0, disp = NaN from the chunk rule)
     assert np.isnan(one["one_" + p + "disp_map"]).any()
+
+
+@pytest.fixture(scope="module")
+def train_ranks(tmp_path_factory):
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    out = str(tmp_path_factory.mktemp("dist_train"))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               WORLD_SIZE=str(WORLD))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_train_worker.py"), out],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(WORLD)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=100)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, (p, log) in enumerate(zip(procs, logs)):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{log[-3000:]}"
+    return [dict(np.load(os.path.join(out, f"train_rank{r}.npz"))) for r in range(WORLD)]
+
+
+def test_data_parallel_train_step_equals_mean_gradient_step(train_ranks):
+    """bench.py's C3 step at world 2 (each rank its own batch and draws, the
+    gradients all-reduced in one flat bucket, then clip + Adam): every rank ends
+    with the same parameters, bit for bit those of one process that averages
+    the two batches' gradients itself before the same Adam step."""
+    ref = train_ranks[0]["ref_params"]
+    for r, rec in enumerate(train_ranks):
+        assert np.array_equal(rec["params"], ref), r
+    assert np.isfinite(ref).all()
