@@ -195,11 +195,11 @@ struct StoreThen {
   Pend& st;
   Split sp;
   template <int G>
-  __device__ __forceinline__ void prefetch() {
-    if constexpr (G == 0) st.template pair<P>(sp.op);
-  }
+  __device__ __forceinline__ void prefetch() {}
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
+    // behind group 0's MFMAs (they issue first), ahead of the slice's pieces
+    if constexpr (G == 0) st.template pair<P>(sp.op);
     sp.template after<G>(acc);
   }
 };
@@ -221,14 +221,13 @@ struct StoreThen2 {   // views slice: pairs P, P+1 stored, then split
   Pend& st;
   Split2 sp;
   template <int G>
-  __device__ __forceinline__ void prefetch() {
-    if constexpr (G == 0) {
+  __device__ __forceinline__ void prefetch() {}
+  template <int G, typename Acc>
+  __device__ __forceinline__ void after(Acc& acc) {
+    if constexpr (G == 0) {   // behind group 0's MFMAs, ahead of the slice's pieces
       st.template pair<P>(sp.a.op);
       st.template pair<P + 1>(sp.b.op);
     }
-  }
-  template <int G, typename Acc>
-  __device__ __forceinline__ void after(Acc& acc) {
     sp.template after<G>(acc);
   }
 };
@@ -906,13 +905,11 @@ struct StoreMaskThen {
   bool loader;          // wave-uniform: this wave stages weight pieces (waves 0-3)
   template <int G>
   __device__ __forceinline__ void prefetch() {
-    if constexpr (G == 0) {
-      if constexpr (P >= 0) st.template pair<P>(sp.op);
-      ms.load();
-    }
+    if constexpr (G == 0) ms.load();
   }
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
+    if constexpr (G == 0 && P >= 0) st.template pair<P>(sp.op);   // behind group 0's MFMAs
     sp.template after<G>(acc);
     if constexpr (G == 7) {
       if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
