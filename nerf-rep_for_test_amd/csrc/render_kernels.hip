@@ -948,6 +948,44 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
   dz[p] = acc;
 }
 
+// L = 10, one wave per coordinate: a block of 3 waves takes 64 samples, wave c
+// sums coordinate c's rows (a third of the loads per thread, so more waves in
+// flight), and lane s of wave 0 adds the three products in c order through LDS
+// (the same operations in the same order as the one-thread-per-sample kernel).
+__global__ __launch_bounds__(192) void freq_encode_fm_backward_dz3_kernel(
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
+    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P,
+    float* __restrict__ dz) {
+  constexpr int L = 10;
+  __shared__ float t3[3][64];
+  const int c = threadIdx.x >> 6, s = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 64 + s;
+  const bool ok = p < P;
+  const int64_t pp = ok ? p : 0;
+  auto de = [&](int row) {
+    float v = d_enc[row * ldd + pp];
+    if (d_enc2) v = v + d_enc2[row * ldd + pp];
+    return v;
+  };
+  float g = de(c);
+#pragma unroll
+  for (int f = 0; f < L; ++f) {
+    const float k = (float)(1 << f);
+    const float sn = enc[(3 + 6 * f + c) * ldd + pp];
+    const float cs = enc[(6 + 6 * f + c) * ldd + pp];
+    const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
+    g = g + ds * k;
+  }
+  t3[c][s] = g * rays_d[(pp / S) * 3 + c];
+  __syncthreads();
+  if (c == 0 && ok) {
+    float acc = t3[0][s];
+    acc = acc + t3[1][s];
+    acc = acc + t3[2][s];
+    dz[p] = acc;
+  }
+}
+
 // max |rgb| / |sigma| of raw [P][4] (float bits: the values are >= 0)
 __global__ __launch_bounds__(256) void raw_absmax_kernel(const float4* __restrict__ raw, int64_t P,
                                                          unsigned* __restrict__ amax) {
@@ -1180,9 +1218,8 @@ int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int
                "nerf_freq_encode_fm_backward_dz: bad size");
   if (P == 0) return 0;
   if (n_freq == 10)   // the xyz encoding (L = 10)
-    hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel<10>, dim3((unsigned)cdiv(P, 256)),
-                       dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P,
-                       n_freq, dz);
+    hipLaunchKernelGGL(freq_encode_fm_backward_dz3_kernel, dim3((unsigned)cdiv(P, 64)),
+                       dim3(192), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P, dz);
   else
     hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel<0>, dim3((unsigned)cdiv(P, 256)),
                        dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P,
