@@ -36,7 +36,11 @@ enum {
 };
 
 const char* nerf_last_error(void);
-int nerf_version(void);                 /* ABI version, bumped on layout changes */
+/* ABI version, bumped on every change of a struct layout or signature below
+ * (2: NerfWgradDesc amax_a2/amax_b2/ldo, NerfX3BwdIO d_raw_t, the
+ * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4) */
+#define NERF_ABI_VERSION 2
+int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
  * source tree this library was compiled from (nerfhip/_lib.py refuses a
  * library whose id differs from the tree beside it; the reference's

@@ -987,12 +987,6 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   // (unwritten) mask words of their tile say, and no max |.| sees them
   float4 dr = io.d_raw[gl];
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  // max |d rgb| and |d sigma| (the heads' wgrad scales, slots 11 / 12): every
-  // lane group holds its samples' d raw, so lane group 0 reports
-  if (g4 == 0) {
-    lds_max_u32(&dmax_lds[11], __float_as_uint(fmaxf(fmaxf(fabsf(dr.x), fabsf(dr.y)), fabsf(dr.z))));
-    lds_max_u32(&dmax_lds[12], __float_as_uint(fabsf(dr.w)));
-  }
   if (io.d_raw_t && g4 == 0 && valid) {   // d raw feature-major: the heads' wgrad operands
     float* t = io.d_raw_t + gs;
     t[0] = dr.w;
@@ -1028,6 +1022,13 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   f32x4 acc[16];
   Op X[8];
   if (first_tile) __syncthreads();   // head, d raw and the three prologue slices resident
+  // max |d rgb| and |d sigma| (the heads' wgrad scales, slots 11 / 12): every
+  // lane group holds its samples' d raw, so lane group 0 reports. After the
+  // first tile's barrier: wave 0's zeroing of the slots (above) must land first
+  if (g4 == 0) {
+    lds_max_u32(&dmax_lds[11], __float_as_uint(fmaxf(fmaxf(fabsf(dr.x), fabsf(dr.y)), fabsf(dr.z))));
+    lds_max_u32(&dmax_lds[12], __float_as_uint(fabsf(dr.w)));
+  }
   load_frags<0>(fp.x, lds_base(R.buf(0), lane));
 
   // ---- d_hv = (W_rgb^T d_rgb) * (hv > 0), NET:68-70 backward, FP32 on the VALU

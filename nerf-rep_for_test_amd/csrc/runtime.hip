@@ -27,7 +27,7 @@ extern "C" {
 
 const char* nerf_last_error(void) { return nerfhip::g_last_error.c_str(); }
 
-int nerf_version(void) { return 1; }
+int nerf_version(void) { return NERF_ABI_VERSION; }
 
 #ifndef NERF_BUILD_ID
 #define NERF_BUILD_ID "unknown"

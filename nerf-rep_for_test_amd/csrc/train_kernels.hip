@@ -646,7 +646,8 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 
 // One Adam step (trainers' torch.optim.Adam, weight decay 0, no amsgrad) over
 // every parameter of the step in ONE launch, the gradient first clamped to
-// [-clip, clip] in place (clip_grad_value_, trainer.py:59; clip <= 0: none),
+// [-clip, clip] in place (clip_grad_value_, trainer.py:59; clip < 0: none,
+// clip 0 zeroes every gradient as clip_grad_value_(0) does),
 // in torch's single-tensor Adam's float32 operation order (lerp, mul +
 // addcmul, addcdiv; the bias corrections in double, as its Python scalars):
 //   m = m + (1 - b1) (g - m),  v = v b2 + (1 - b2) g g,
@@ -656,7 +657,7 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 constexpr int kAdamMax = 64;
 constexpr int kAdamPer = 4;                 // elements per thread, loaded together
 constexpr int kAdamBlock = 256 * kAdamPer;  // elements per workgroup (~1 200 workgroups for
-                                            // both networks: as many finish-counter atomics)
+                                            // both networks)
 struct AdamBatch {
   NerfAdamTensor t[kAdamMax];
   int blk_end[kAdamMax];           // prefix sums of the tensors' workgroups

@@ -10,6 +10,7 @@ import os
 import threading
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ABI_VERSION = 2   # include/nerfhip.h NERF_ABI_VERSION
 LIB_PATH = os.environ.get("NERFHIP_LIB", os.path.join(PKG_ROOT, "lib", "libnerfhip.so"))
 
 MLP_SLICES = 73
@@ -134,6 +135,12 @@ def lib():
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args
+            # the struct layouts and signatures of SIGNATURES are those of ABI_VERSION:
+            # enforced for every library, NERFHIP_LIB variants included
+            ver = h.nerf_version()
+            if ver != ABI_VERSION:
+                raise NerfHipError(f"{LIB_PATH} has ABI version {ver}, this module speaks "
+                                   f"{ABI_VERSION} (include/nerfhip.h NERF_ABI_VERSION)")
             want = tree_build_id()
             got = h.nerf_build_id().decode()
             # NERFHIP_LIB points at a deliberately different build (timing-only

@@ -280,15 +280,15 @@ class NerfTrainer:
         self.adam = adam
         if adam == "hip":
             from .adam import HipAdam
-            self.opt = HipAdam(self.parameters(), lr=lr, eps=1e-8, clip=self.clip_value)
+            self.opt = HipAdam(self.trained_parameters(), lr=lr, eps=1e-8, clip=self.clip_value)
         elif adam == "capturable":
-            self.opt = torch.optim.Adam(self.parameters(),
+            self.opt = torch.optim.Adam(self.trained_parameters(),
                                         lr=torch.tensor(lr, device=self.device), eps=1e-8,
                                         weight_decay=0.0, capturable=True, foreach=True)
         else:
             # one fused multi-tensor Adam kernel per step on the GPU
-            self.opt = torch.optim.Adam(self.parameters(), lr=lr, eps=1e-8, weight_decay=0.0,
-                                        fused=self.device.type == "cuda")
+            self.opt = torch.optim.Adam(self.trained_parameters(), lr=lr, eps=1e-8,
+                                        weight_decay=0.0, fused=self.device.type == "cuda")
         self._graphs = {}
         self._one = {}
         self._warm = {}
@@ -296,6 +296,12 @@ class NerfTrainer:
 
     def parameters(self):
         return list(self.coarse.parameters()) + list(self.fine.parameters())
+
+    def trained_parameters(self):
+        """The parameters a step updates: without a fine pass (N_importance 0,
+        VR:181) the fine network takes no part and gets no gradient."""
+        return list(self.coarse.parameters()) + (list(self.fine.parameters())
+                                                 if self.N_importance > 0 else [])
 
     def named_parameters(self):
         for prefix, m in (("model", self.coarse), ("model_fine", self.fine)):
@@ -401,10 +407,10 @@ class NerfTrainer:
         if one is None:   # d loss / d loss = 1, kept (no fill kernel per step)
             one = self._one[loss.device] = torch.ones((), device=loss.device, dtype=loss.dtype)
         loss.backward(one)
-        if group is not None:   # parameters without a gradient (e.g. no fine pass) skipped
-            allreduce_mean([p.grad for p in self.parameters() if p.grad is not None], group)
+        if group is not None:
+            allreduce_mean([p.grad for p in self.trained_parameters()], group)
         if self.adam != "hip":   # (HipAdam clamps the gradients itself, in place)
-            torch.nn.utils.clip_grad_value_(self.parameters(), self.clip_value)
+            torch.nn.utils.clip_grad_value_(self.trained_parameters(), self.clip_value)
         self.opt.step()
         return losses
 

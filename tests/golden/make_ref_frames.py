@@ -36,6 +36,21 @@ reference's source is stored - only numbers it produced.
     python tests/golden/make_ref_frames.py r0_c2_frame0
     python tests/golden/make_ref_frames.py --add-gt   # store the GT PNG in older files
     python tests/golden/make_ref_frames.py --zall     # zh_<name>.npz, see below
+    python tests/golden/make_ref_frames.py --dump r3_c4_yaml_frame24   # a new frame + its zh
+    python tests/golden/make_ref_frames.py --tail <name> <cand_*.npz...>   # zt_<name>.npz
+
+r3_c4_yaml_frame24 also stores ``grid_init_bits``: the Renderer's own grid as
+drawn at construction (the test regenerates it through the plugin from the
+same seed and must find it equal).
+
+``--zall`` and ``--dump`` also keep, outside the fixtures (``.scratch/``, never
+committed), every ray's coarse depths and coarse weights as the reference's
+fine sampling consumed them (VR:181-182). ``--tail`` cuts from them the rows of
+the pixels that the GPU frame test lists as near or beyond tolerance
+(``NERF_FRAME_DUMP``): ``tests/golden/zt_<name>.npz`` (pixels, z_coarse,
+w_coarse). test_gpu_frames.py re-derives each of those pixels' fine rows with
+the oracle's ``sample_fine`` (hash-checked against zh), renders the fine pass
+on them with HIP and holds it to 1e-5.
 
 ``--zall`` renders each frame again (asserting every map equals the stored
 one) and writes ``tests/golden/zh_<name>.npz``: the reference's disp maps
@@ -72,7 +87,16 @@ FRAMES = {
     "r1_c2_frame8_pert": dict(frame=8, perturb=1, ess=False, ert=False, seed=RSEED),
     "r2_c4_frame16": dict(frame=16, perturb=0, ess=True, ert=True, thr=0.01,
                           grid=(0, 128, 1.2, 0.1), counter=0),
+    # lego.yaml's own eval configuration (run.py --type evaluate): perturb 1
+    # (lego.yaml:22), ESS + ERT at 0.01 (:96-99), the Renderer's OWN occupancy
+    # grid (VR:67, :857-864: sphere | torch.rand < 0.1, drawn at construction
+    # right after torch.manual_seed(seed)), its counter from 0 (VR:63), then the
+    # per-chunk perturb draws of the ESS sampler (VR:1080-1085) from the same
+    # generator
+    "r3_c4_yaml_frame24": dict(frame=24, perturb=1, ess=True, ert=True, thr=0.01,
+                               seed=RSEED + 3, grid="own", counter=0),
 }
+SCRATCH = os.path.join(REPO, ".scratch")
 
 
 def _import_reference():
@@ -115,7 +139,57 @@ def psnr(pred, gt):
     return float(-10.0 * np.log10(mse))
 
 
-def capture(name, spec, cfg, Network, vr, meta):
+class _Recorder:
+    """Wraps the Renderer's composite (VR:286-357 / VR:1089-1157) to record, per
+    ray, the coarse depths and the coarse weights the fine sampling consumed
+    (VR:181-182), the fine rows' hash (VR:183) and, with ERT, each call's
+    chunk-wide decision (VR:1116)."""
+
+    def __init__(self, rend):
+        import torch
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from goldlib import row_hash
+        self.rend = rend
+        self.zc, self.wc, self.hashes, self.chunk_any = [], [], [], []
+        name = "_raw2outputs_with_ert" if rend.enable_ert else "_raw2outputs"
+        orig = getattr(rend, name)
+        calls = {"n": 0}
+
+        def rec(raw, z, rays_d):
+            r = orig(raw, z, rays_d)
+            if rend.enable_ert:
+                d = torch.cat([z[..., 1:] - z[..., :-1], torch.full_like(z[..., :1], 1e10)], -1)
+                d = d * torch.norm(rays_d[..., None, :], dim=-1)
+                a = 1. - torch.exp(-torch.relu(raw[..., 3]) * d)
+                sh = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
+                self.chunk_any.append(bool((torch.cumprod(1.0 - sh, 1) < rend.ert_threshold).any()))
+            if calls["n"] % 2 == 0:     # coarse call: its depths and weights (VR:181-182)
+                self.zc.append(z.detach().numpy().astype(np.float32))
+                self.wc.append(r[3].detach().numpy().astype(np.float32))
+            else:                       # fine call (VR:190-193)
+                self.hashes.append(row_hash(z.detach().numpy()))
+            calls["n"] += 1
+            return r
+        setattr(rend, name, rec)
+
+    def save(self, name, ret):
+        """zh_<name>.npz (tests/golden) and the full per-ray coarse rows under
+        .scratch/ (328 MB per frame, never committed: `--tail` extracts the
+        pixels a fixture needs)."""
+        zh = np.concatenate(self.hashes)
+        path = os.path.join(OUT, f"zh_{name}.npz")
+        np.savez_compressed(path, zall_hash=zh, chunk_any=np.array(self.chunk_any, bool),
+                            disp_map=ret["disp_map"].numpy().astype(np.float32),
+                            disp_map_0=ret["disp_map_0"].numpy().astype(np.float32),
+                            ckpt_sha256=ckpt_sha())
+        os.makedirs(SCRATCH, exist_ok=True)
+        np.save(os.path.join(SCRATCH, f"zc_{name}.npy"), np.concatenate(self.zc))
+        np.save(os.path.join(SCRATCH, f"wc_{name}.npy"), np.concatenate(self.wc))
+        np.save(os.path.join(SCRATCH, f"zh_{name}.npy"), zh)
+        print(f"{path}; coarse rows in {SCRATCH}", flush=True)
+
+
+def capture(name, spec, cfg, Network, vr, meta, dump=False):
     import torch
     cfg.task_arg.N_importance = 128
     cfg.task_arg.perturb = spec["perturb"]
@@ -128,11 +202,19 @@ def capture(name, spec, cfg, Network, vr, meta):
     sd = torch.load(CKPT, map_location="cpu", weights_only=True)["net"]
     net.load_state_dict(sd)
     net.eval()
+    own = spec.get("grid") == "own"
+    if own:   # the Renderer's own grid draw consumes the seeded generator first
+        torch.manual_seed(spec["seed"])
     rend = vr.Renderer(net)
     rend.use_cuda_kernels = False
-    if "grid" in spec:
+    extra = {}
+    if own:
+        extra["grid_init_bits"] = np.packbits(rend.occupancy_grid.numpy().reshape(-1))
+        assert rend.grid_update_counter == spec["counter"]
+    elif "grid" in spec:
         rend.occupancy_grid = torch.from_numpy(make_occupancy_grid(*spec["grid"]).copy())
         rend.grid_update_counter = spec["counter"]
+    rec = _Recorder(rend) if dump else None
     H = W = 800
     angle = float(meta["camera_angle_x"])
     focal = 0.5 * W / np.tan(0.5 * angle)                       # blender.py:41-42
@@ -140,7 +222,7 @@ def capture(name, spec, cfg, Network, vr, meta):
     K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
     batch = {"H": H, "W": W, "pose": torch.from_numpy(pose)[None],
              "intrinsics": torch.from_numpy(K)[None]}
-    if "seed" in spec:
+    if "seed" in spec and not own:
         torch.manual_seed(spec["seed"])
     t0 = time.time()
     with torch.no_grad():
@@ -148,7 +230,8 @@ def capture(name, spec, cfg, Network, vr, meta):
     dt = time.time() - t0
     out = {k: v.numpy().astype(np.float32) for k, v in ret.items() if not k.startswith("disp")}
     gt = gt_image(spec["frame"])
-    extra = {}
+    if rec is not None:
+        rec.save(name, ret)
     if "grid" in spec:
         extra["grid_final_bits"] = np.packbits(rend.occupancy_grid.numpy().reshape(-1))
         extra["grid_counter_final"] = np.int64(rend.grid_update_counter)
@@ -157,8 +240,9 @@ def capture(name, spec, cfg, Network, vr, meta):
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), pose=pose, K=K, H=H, W=W,
                         frame=spec["frame"], perturb=spec["perturb"],
                         seed=spec.get("seed", -1), ess=spec["ess"], ert=spec["ert"],
-                        thr=spec.get("thr", 0.0), grid_spec=np.array(spec.get("grid", ()),
-                                                                      np.float64),
+                        thr=spec.get("thr", 0.0),
+                        grid_spec=np.array(() if own else spec.get("grid", ()), np.float64),
+                        grid_own=own,
                         counter0=spec.get("counter", -1), psnr_ref=p, psnr_ref_0=p0,
                         cpu_seconds=dt, torch_threads=torch.get_num_threads(),
                         gt_png=gt_png(spec["frame"]), ckpt_sha256=ckpt_sha(),
@@ -168,10 +252,10 @@ def capture(name, spec, cfg, Network, vr, meta):
 
 
 def capture_zall(name, spec, cfg, Network, vr, meta):
-    """Re-render `name` with the fine composite's depths hashed per ray."""
+    """Re-render `name` (asserting every stored map bit for bit), write its
+    zh_<name>.npz if missing (asserting the stored hashes otherwise) and the
+    per-ray coarse rows under .scratch/ (_Recorder)."""
     import torch
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from goldlib import row_hash
     cfg.task_arg.N_importance = 128
     cfg.task_arg.perturb = spec["perturb"]
     cfg.task_arg.lindisp = False
@@ -182,37 +266,24 @@ def capture_zall(name, spec, cfg, Network, vr, meta):
     net = Network()
     net.load_state_dict(torch.load(CKPT, map_location="cpu", weights_only=True)["net"])
     net.eval()
+    own = spec.get("grid") == "own"
+    if own:
+        torch.manual_seed(spec["seed"])
     rend = vr.Renderer(net)
     rend.use_cuda_kernels = False
-    if "grid" in spec:
+    if "grid" in spec and not own:
         rend.occupancy_grid = torch.from_numpy(make_occupancy_grid(*spec["grid"]).copy())
         rend.grid_update_counter = spec["counter"]
-    comp_name = "_raw2outputs_with_ert" if rend.enable_ert else "_raw2outputs"
-    orig_c = getattr(rend, comp_name)
-    calls = {"n": 0}
-    hashes, chunk_any = [], []
-
-    def rec_c(raw, z, rays_d):
-        r = orig_c(raw, z, rays_d)
-        if rend.enable_ert:          # VR:1104-1116, the chunk-wide decision of this call
-            d = torch.cat([z[..., 1:] - z[..., :-1], torch.full_like(z[..., :1], 1e10)], -1)
-            d = d * torch.norm(rays_d[..., None, :], dim=-1)
-            a = 1. - torch.exp(-torch.relu(raw[..., 3]) * d)
-            sh = torch.cat([torch.zeros_like(a[:, :1]), a[:, :-1]], 1)
-            chunk_any.append(bool((torch.cumprod(1.0 - sh, 1) < rend.ert_threshold).any()))
-        if calls["n"] % 2 == 1:      # fine call of the chunk (VR:190-193)
-            hashes.append(row_hash(z.detach().numpy()))
-        calls["n"] += 1
-        return r
-
-    setattr(rend, comp_name, rec_c)
+    zh_path = os.path.join(OUT, f"zh_{name}.npz")
+    old_zh = dict(np.load(zh_path)) if os.path.exists(zh_path) else None
+    rec = _Recorder(rend)
     H = W = 800
     focal = 0.5 * W / np.tan(0.5 * float(meta["camera_angle_x"]))
     pose = np.array(meta["frames"][spec["frame"]]["transform_matrix"], np.float32)
     K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
     batch = {"H": H, "W": W, "pose": torch.from_numpy(pose)[None],
              "intrinsics": torch.from_numpy(K)[None]}
-    if "seed" in spec:
+    if "seed" in spec and not own:
         torch.manual_seed(spec["seed"])
     t0 = time.time()
     with torch.no_grad():
@@ -222,14 +293,42 @@ def capture_zall(name, spec, cfg, Network, vr, meta):
     for k, v in ret.items():
         if not k.startswith("disp"):
             assert np.array_equal(v.numpy(), old["out_" + k]), (name, k)
-    zh = np.concatenate(hashes)
+    zh = np.concatenate(rec.hashes)
     assert zh.shape == (H * W,), zh.shape
-    path = os.path.join(OUT, f"zh_{name}.npz")
-    np.savez_compressed(path, zall_hash=zh, chunk_any=np.array(chunk_any, bool),
-                        disp_map=ret["disp_map"].numpy().astype(np.float32),
-                        disp_map_0=ret["disp_map_0"].numpy().astype(np.float32),
+    if old_zh is not None:
+        assert np.array_equal(zh, old_zh["zall_hash"]), name
+        assert np.array_equal(np.array(rec.chunk_any, bool), old_zh["chunk_any"]), name
+    rec.save(name, ret)
+    print(f"{name}: re-rendered in {dt:.0f} s", flush=True)
+
+
+def capture_tail(name, cand_files):
+    """tests/golden/zt_<name>.npz: for the pixels the GPU frame test listed as
+    near or beyond tolerance (tests/test_gpu_frames.py NERF_FRAME_DUMP, every
+    precision's file), the reference's coarse depths and coarse weights from
+    .scratch/ (the rows its fine sampling consumed, VR:181-182). The oracle's
+    _sample_fine + merge of those rows (VR:239-268, :183) must give the
+    reference's own fine-row hash for every pixel (asserted here, and again in
+    the test)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    sys.path.insert(0, REPO)
+    from goldlib import row_hash
+    from oracle import nerf_oracle as O
+    pix = np.unique(np.concatenate([np.load(f)["pixels"] for f in cand_files])).astype(np.int64)
+    zc = np.load(os.path.join(SCRATCH, f"zc_{name}.npy"), mmap_mode="r")
+    wc = np.load(os.path.join(SCRATCH, f"wc_{name}.npy"), mmap_mode="r")
+    zh = np.load(os.path.join(OUT, f"zh_{name}.npz"))["zall_hash"]
+    z = np.ascontiguousarray(zc[pix])
+    w = np.ascontiguousarray(wc[pix])
+    mids = (np.float32(0.5) * (z[:, 1:] + z[:, :-1])).astype(np.float32)
+    zf = O.sample_fine(mids, w[:, 1:-1], O.linspace_f32(0.0, 1.0, 128))
+    zall = np.sort(np.concatenate([z, zf], -1), -1)
+    bad = int((row_hash(zall) != zh[pix]).sum())
+    assert bad == 0, f"{name}: {bad} of {len(pix)} oracle fine rows differ from the reference's"
+    path = os.path.join(OUT, f"zt_{name}.npz")
+    np.savez_compressed(path, pixels=pix.astype(np.int32), z_coarse=z, w_coarse=w,
                         ckpt_sha256=ckpt_sha())
-    print(f"{path}: {os.path.getsize(path) / 1e6:.1f} MB, {dt:.0f} s", flush=True)
+    print(f"{path}: {len(pix)} pixels, {os.path.getsize(path) / 1e6:.2f} MB", flush=True)
 
 
 def add_gt(name):
@@ -248,13 +347,20 @@ def main(argv):
         for n in argv[1:] or list(FRAMES):
             add_gt(n)
         return
+    if argv and argv[0] == "--tail":     # --tail <name> <cand npz files...>
+        capture_tail(argv[1], argv[2:])
+        return
     zall = "--zall" in argv
-    argv = [a for a in argv if a != "--zall"]
+    dump = "--dump" in argv
+    argv = [a for a in argv if a not in ("--zall", "--dump")]
     cfg, Network, vr = _import_reference()
     meta = json.load(open(os.path.join(REF, "data/nerf_synthetic/lego/transforms_test.json")))
     names = argv or list(FRAMES)
     for n in names:
-        (capture_zall if zall else capture)(n, FRAMES[n], cfg, Network, vr, meta)
+        if zall:
+            capture_zall(n, FRAMES[n], cfg, Network, vr, meta)
+        else:
+            capture(n, FRAMES[n], cfg, Network, vr, meta, dump=dump)
 
 
 if __name__ == "__main__":

@@ -164,6 +164,15 @@ def _check(name, prec, z, got, zall_hip, extra=None):
         np.logical_or.at(cd, ch, ddiff)
         expl |= cd[ch]
     unexpl = tail & ~expl
+    dump = os.environ.get("NERF_FRAME_DUMP")
+    if dump:   # the pixels near or beyond tolerance (the capture list of make_ref_frames --tail)
+        ratio = np.max(np.stack([np.where(np.isfinite(e), e, 1e30) / tol
+                                 for e, tol in fine.values()]), 0)
+        pix = np.flatnonzero(ratio > 0.25)
+        os.makedirs(dump, exist_ok=True)
+        np.savez_compressed(os.path.join(dump, f"cand_{name}_{prec}.npz"), pixels=pix,
+                            ratio=ratio[pix].astype(np.float32), tail=tail[pix],
+                            ddiff=ddiff[pix])
     nan_ref = np.isnan(zh["disp_map"].reshape(n))
     rep = {"frame": name, "precision": prec, "pixels": n,
            "psnr_ref_vs_gt": p_ref, "psnr_hip_vs_gt": p_hip, "dpsnr": p_hip - p_ref,

@@ -156,6 +156,24 @@ def test_steps_reduce_loss(dev, mlp):
         assert p.grad is None or p.grad.abs().max() <= 40.0
 
 
+@pytest.mark.parametrize("adam", ["hip", "capturable"])
+def test_coarse_only_steps(dev, adam):
+    """N_importance = 0 (VR:181: no fine pass): the fine network takes no part,
+    gets no gradient and is left untouched; the coarse one trains."""
+    from nerfhip.train import NerfTrainer
+    z = load("t1_train_step")
+    tr = NerfTrainer(dev, params_of(z), N_importance=0, adam=adam)
+    _, _, ro, rd, t_rand, _, gt = _setup(dev)
+    fine0 = [p.detach().clone() for p in tr.fine.parameters()]
+    first = tr.step(ro, rd, gt, t_rand)["loss"].item()
+    for _ in range(20):
+        last = tr.step(ro, rd, gt, t_rand)["loss"].item()
+    assert np.isfinite(first) and last < 0.9 * first
+    assert all(p.grad is None for p in tr.fine.parameters())
+    assert all(torch.equal(a, b) for a, b in zip(fine0, tr.fine.parameters()))
+    assert all(p.grad is not None for p in tr.coarse.parameters())
+
+
 # ------------------------------------------------------------------ the plugin
 def _plugin_train_render(dev, name, mlp):
     """Renderer(net).render(batch) in training mode, as trainers/nerf.py:20-37
