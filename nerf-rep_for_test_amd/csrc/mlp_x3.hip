@@ -425,8 +425,16 @@ __device__ __forceinline__ int enc_dir_row(int g, int j) {
   return 28 + g;
 }
 
+// The range check of a raw buffer access covers voffset + soffset + the
+// instruction offset, and drops an access that straddles num_records
+// (tools/probe/buffer_range.hip on gfx950). So the samples past P are dropped by
+// voffset 0x7fffffff whatever row offset rides in soffset (rows * ld * 4 < 2^31
+// is enforced by the launchers: the sum cannot wrap), and a null output (the
+// skipped feature / DF rows) gets num_records 0: every store through it is
+// dropped even if a path forgets the ActStore::on test.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, int64_t ld) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)((int64_t)rows * ld * 4), 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, p ? (int)((int64_t)rows * ld * 4) : 0,
+                                           0x00020000);
 }
 
 // LIST: the samples are the flat indices list[0 .. *count) (ray * S + step,
@@ -1010,10 +1018,12 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     st.valid = valid;
     return st;
   };
+  // the bit words of whole 128-sample tiles (relu_bits_words): 4 KiB per tile
+  const int mask_bytes = (int)(ntiles * 8 * 4 * 64 * 2);
   auto mask_for = [&](int L) {
     int li = L;
     asm volatile("" : "+s"(li));
-    return MaskSrc{__builtin_amdgcn_make_buffer_rsrc((void*)io.bits[li], 0, 0x7fffffff, 0x00020000),
+    return MaskSrc{__builtin_amdgcn_make_buffer_rsrc((void*)io.bits[li], 0, mask_bytes, 0x00020000),
                    (unsigned)(((tile * 8 + wave) * 4 * 64) * 2), mask_lds + wave * 128};
   };
   auto amax_to_lds = [&](int slot, float mx) { lds_max_u32(&dmax_lds[slot], __float_as_uint(mx)); };

@@ -97,6 +97,7 @@ FRAMES = {
                                seed=RSEED + 3, grid="own", counter=0),
 }
 SCRATCH = os.path.join(REPO, ".scratch")
+TAIL_MARGIN = 0.5     # --tail keeps the pixels beyond this fraction of the tolerance
 
 
 def _import_reference():
@@ -314,7 +315,10 @@ def capture_tail(name, cand_files):
     sys.path.insert(0, REPO)
     from goldlib import row_hash
     from oracle import nerf_oracle as O
-    pix = np.unique(np.concatenate([np.load(f)["pixels"] for f in cand_files])).astype(np.int64)
+    def near(f):   # beyond half the tolerance in that run, or in its tail
+        c = np.load(f)
+        return c["pixels"][(c["ratio"] > TAIL_MARGIN) | c["tail"]]
+    pix = np.unique(np.concatenate([near(f) for f in cand_files])).astype(np.int64)
     zc = np.load(os.path.join(SCRATCH, f"zc_{name}.npy"), mmap_mode="r")
     wc = np.load(os.path.join(SCRATCH, f"wc_{name}.npy"), mmap_mode="r")
     zh = np.load(os.path.join(OUT, f"zh_{name}.npz"))["zall_hash"]

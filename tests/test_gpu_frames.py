@@ -111,6 +111,112 @@ def _pix_err(got, ref, kind):
     return e, tol
 
 
+def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
+    """Every tail pixel (beyond tolerance and beyond 4x the reference's own
+    spread) re-rendered on the reference's OWN fine depths.
+
+    tests/golden/zt_<name>.npz (make_ref_frames.py --tail) holds, for the pixels
+    the frame test lists near or beyond tolerance, the coarse depths and coarse
+    weights the reference's fine sampling consumed (VR:181-182). Here the
+    oracle's ``sample_fine`` + merge (VR:239-268, :183) turns them into the fine
+    rows, whose hash must equal the reference's own (zh, VR:183) -- so the rows
+    ARE the reference's -- and the HIP fine MLP + composite (this precision) on
+    exactly those rows must give the reference's maps within 1e-5 (rgb / acc
+    abs, depth 1e-5 max(1, |d|), disp 1e-4 relative where acc > 1e-6). With ERT
+    the composite runs each reference chunk's tail rays in a 2048-ray slot of
+    their own, with that chunk's decision (VR:1116, zh chunk_any of its fine
+    call) restored by a terminating stand-in ray when the reference's chunk
+    terminated, so the argmax rule (VR:1115-1123) acts as it did there."""
+    from nerfhip.render import NerfPipeline
+    from oracle import nerf_oracle as O
+    H, W = int(z["H"]), int(z["W"])
+    n = H * W
+    path = os.path.join(GOLDEN, f"zt_{name}.npz")
+    assert os.path.exists(path), f"{path} missing: make_ref_frames.py --tail"
+    zt = np.load(path)
+    P = zt["pixels"].astype(np.int64)
+    tail_pix = np.asarray(tail_pix, np.int64)
+    pos = np.minimum(np.searchsorted(P, tail_pix), len(P) - 1)
+    cap = P[pos] == tail_pix
+    T, rows = tail_pix[cap], pos[cap]
+    rep = {"tail_captured": int(cap.sum()), "tail_uncaptured": int((~cap).sum()),
+           "tail_uncaptured_pixels": tail_pix[~cap][:20].tolist(),
+           "tail_oracle_hash_mismatch": 0, "tail_given_ref_depths_max_err": {},
+           "tail_given_ref_depths_max_ratio": 0.0}
+    if len(T) == 0:
+        return rep
+    zc = np.ascontiguousarray(zt["z_coarse"][rows])
+    wc = np.ascontiguousarray(zt["w_coarse"][rows])
+    mids = (np.float32(0.5) * (zc[:, 1:] + zc[:, :-1])).astype(np.float32)
+    zf = O.sample_fine(mids, wc[:, 1:-1], O.linspace_f32(0.0, 1.0, 128))
+    zall = np.ascontiguousarray(np.sort(np.concatenate([zc, zf], -1), -1), np.float32)
+    rep["tail_oracle_hash_mismatch"] = int((row_hash(zall) != zh["zall_hash"][T]).sum())
+    dev = torch.device("cuda:0")
+    ert = bool(z["ert"])
+    pipe = NerfPipeline(dev, N_samples=64, N_importance=128, enable_ert=ert,
+                        ert_threshold=float(z["thr"]) if ert else 0.01, mlp_precision=prec)
+    pipe.load_checkpoint(CKPT_DIR)
+    ro, rd = pipe.camera_rays(H, W, z["pose"], z["K"])
+    idx = torch.from_numpy(T).to(dev)
+    ro_t, rd_t = ro[idx].contiguous(), rd[idx].contiguous()
+    S2 = zall.shape[1]
+    z_t = torch.from_numpy(zall).to(dev)
+    m = len(T)
+    raw = pipe.mlp(pipe.fine, ro_t, rd_t, z_t, S2, m, S2)      # full evaluation, no compaction
+    if not ert:
+        out = pipe.alloc_outputs(m)["coarse"]
+        pipe.composite(raw, z_t, S2, rd_t, m, S2, out, 0, need_weights=False)
+        got = [o.cpu().numpy() for o in out]
+    else:
+        ch = T // REF_CHUNK
+        uch, inv, cnt = np.unique(ch, return_inverse=True, return_counts=True)
+        assert cnt.max() < REF_CHUNK     # room for the stand-in ray in every slot
+        first = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+        order = np.argsort(inv, kind="stable")
+        rank = np.empty(m, np.int64)
+        rank[order] = np.arange(m) - first[inv[order]]
+        slot = inv * REF_CHUNK + rank
+        N = len(uch) * REF_CHUNK
+        raw_p = torch.zeros((N, S2, 4), device=dev, dtype=torch.float32)
+        z_p = z_t[:1].expand(N, S2).contiguous()
+        rd_p = rd_t[:1].expand(N, 3).contiguous()
+        sl = torch.from_numpy(slot).to(dev)
+        raw_p[sl] = raw.view(m, S2, 4)
+        z_p[sl] = z_t
+        rd_p[sl] = rd_t
+        decided = zh["chunk_any"][2 * uch + 1]          # the fine call of each chunk
+        dummy = torch.from_numpy((np.flatnonzero(decided) * REF_CHUNK
+                                  + cnt[decided]).astype(np.int64)).to(dev)
+        raw_p[dummy, :, 3] = 1e4                         # terminates at its first sample
+        out = pipe.alloc_outputs(N)["coarse"]
+        pipe.composite(raw_p.view(N * S2, 4), z_p, S2, rd_p, N, S2, out, 0, need_weights=False)
+        got = [o[sl].cpu().numpy() for o in out]
+        rep["tail_ert_chunks"] = int(len(uch))
+        rep["tail_ert_chunks_terminated"] = int(decided.sum())
+    ref_rgb = z["out_rgb_map"].reshape(n, 3)[T].astype(np.float64)
+    ref_acc = z["out_acc_map"].reshape(n)[T].astype(np.float64)
+    ref_depth = z["out_depth_map"].reshape(n)[T].astype(np.float64)
+    ref_disp = zh["disp_map"].reshape(n)[T].astype(np.float64)
+    g_rgb, g_disp, g_acc, g_depth = (np.asarray(a, np.float64) for a in got)
+    e = {"rgb": np.abs(g_rgb - ref_rgb).max(-1), "acc": np.abs(g_acc - ref_acc),
+         "depth": np.abs(g_depth - ref_depth)}
+    tol = {"rgb": np.full(m, TOL), "acc": np.full(m, TOL),
+           "depth": TOL * np.maximum(1.0, np.abs(ref_depth))}
+    mass = (ref_acc > 1e-6) | (g_acc > 1e-6)
+    with np.errstate(invalid="ignore"):
+        de = np.abs(g_disp - ref_disp)
+    de = np.where(np.isnan(g_disp) != np.isnan(ref_disp), np.inf, np.nan_to_num(de, nan=0.0))
+    e["disp"] = np.where(mass, de, 0.0)
+    tol["disp"] = 1e-4 * np.maximum(1e-3, np.nan_to_num(np.abs(ref_disp), nan=0.0))
+    ratio = np.max(np.stack([e[k] / tol[k] for k in e]), 0)
+    rep["tail_given_ref_depths_max_err"] = {k: float(v.max()) for k, v in e.items()}
+    rep["tail_given_ref_depths_max_ratio"] = float(ratio.max())
+    rep["tail_given_ref_depths_over_tol"] = [
+        {"pixel": int(T[i]), **{k: float(e[k][i]) for k in e}}
+        for i in np.flatnonzero(ratio > 1.0)[:20]]
+    return rep
+
+
 def _check(name, prec, z, got, zall_hip, extra=None):
     H, W = int(z["H"]), int(z["W"])
     n = H * W
@@ -206,6 +312,7 @@ def _check(name, prec, z, got, zall_hip, extra=None):
                 "depth_hip": float(got["depth_map"].reshape(n)[i]),
                 **{f"{k}_err": float(e[i]) for k, (e, _) in fine.items()}}
                for i in np.flatnonzero(unexpl)[:20]],
+           **_tail_given_reference_depths(name, prec, z, zh, np.flatnonzero(tail)),
            "psnr_hip_vs_ref": float("inf") if mse == 0 else -10 * np.log10(mse),
            "reference_cpu_seconds": float(z["cpu_seconds"])}
     if extra:
@@ -224,6 +331,10 @@ def _check(name, prec, z, got, zall_hip, extra=None):
     assert rep["fine_rgb_frac_within_tol"] >= FRAC, rep
     assert rep["fine_frac_within_tol_or_4x_ref_spread"] >= FRAC_ALL, rep
     assert rep["tail_unexplained"] == 0, rep
+    # the whole tail, on the reference's own depths (verdict r4 item 1)
+    assert rep["tail_uncaptured"] == 0, rep
+    assert rep["tail_oracle_hash_mismatch"] == 0, rep
+    assert rep["tail_given_ref_depths_max_ratio"] <= 1.0, rep
     assert rep["psnr_hip_vs_ref"] >= 60.0, rep
     return rep
 
@@ -314,4 +425,64 @@ def test_c4_frame16_vs_reference(dev, prec):
                   "evaluated_sample_frac": ev / max(full, 1)})
     assert rep["disp_nan_ref"] > 0, rep          # the frame exercises quirk 1 / acc = 0
     assert pipe.grid_update_counter == int(z["grid_counter_final"]), rep
+    assert grid_ok, rep
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "fp32"])
+def test_lego_yaml_eval_frame_through_plugin(dev, prec):
+    """lego.yaml's own eval configuration (run.py --type evaluate; lego.yaml:22,
+    :96-99): perturb 1, ESS + ERT at 0.01, the Renderer's OWN occupancy grid
+    (VR:67, :857-864, drawn at construction) and its counter from 0 (VR:63), so
+    the call-0 and call-500 grid self-updates (VR:1147-1155) fall inside the
+    frame, then the ESS sampler's per-chunk perturb draws (VR:1080-1085) -- all
+    from torch's CPU generator seeded as the capture was (make_ref_frames.py
+    r3_c4_yaml_frame24), replayed through the drop-in plugin."""
+    from src.config import cfg, reset
+    from src.models.nerf.network import Network
+    from src.models.nerf.renderer.volume_renderer import Renderer
+    z = _frame("r3_c4_yaml_frame24")
+    n = int(z["H"]) * int(z["W"])
+    reset()
+    cfg.task_arg.perturb = 1
+    cfg.enable_ess = True
+    cfg.enable_ert = True
+    cfg.ert_threshold = float(z["thr"])
+    cfg.mlp_precision = prec
+    net = Network().to(dev)
+    sd = torch.load(os.path.join(CKPT_DIR, "latest.pth"), map_location="cpu",
+                    weights_only=True)["net"]
+    net.load_state_dict(sd)
+    net.eval()
+    gen = torch.Generator().manual_seed(int(z["seed"]))
+    sizes = []
+    orig = torch.rand
+
+    def rand(size, *a, device=None, **kw):
+        sizes.append(tuple(size))
+        return orig(size, generator=gen).to(device)
+    torch.rand = rand
+    try:
+        rend = Renderer(net)        # draws its grid (VR:861)
+        grid0 = np.packbits(rend.occupancy_grid.cpu().numpy().reshape(-1))
+        assert np.array_equal(grid0, z["grid_init_bits"]), "the Renderer's own grid differs"
+        assert rend.grid_update_counter == int(z["counter0"]) == 0
+        batch = {"H": int(z["H"]), "W": int(z["W"]),
+                 "pose": torch.from_numpy(z["pose"])[None],
+                 "intrinsics": torch.from_numpy(z["K"])[None]}
+        rend.pipeline.capture_zall = []
+        with torch.no_grad():
+            out = rend.render(batch)
+    finally:
+        torch.rand = orig
+        reset()
+    assert sizes == [(128, 128, 128)] + [(min(2048, n - c), 64) for c in range(0, n, 2048)]
+    ev, full = rend.pipeline.evaluated_samples()
+    grid_ok = np.array_equal(np.packbits(rend.occupancy_grid.cpu().numpy().reshape(-1)),
+                             z["grid_final_bits"])
+    rep = _check("r3_c4_yaml_frame24", prec, z, {k: v.cpu().numpy() for k, v in out.items()},
+                 _zall(rend.pipeline),
+                 {"grid_init_equal": True, "grid_final_equal": bool(grid_ok),
+                  "counter": rend.grid_update_counter,
+                  "evaluated_sample_frac": ev / max(full, 1)})
+    assert rend.grid_update_counter == int(z["grid_counter_final"]), rep
     assert grid_ok, rep

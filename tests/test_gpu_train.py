@@ -13,6 +13,8 @@ of its network, most other tensors by < 0.1 %).
 The same math on the CPU matches the reference to 1e-5 (tests/test_train.py).
 Both MLP back ends are held to the same bounds: the x3 MFMA kernels
 (train_mlp.py, the default) and torch modules on hipBLASLt FP32 GEMMs."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -20,6 +22,7 @@ import torch
 from goldlib import load, max_err, params_of, psnr
 
 pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -465,3 +468,42 @@ def test_hip_adam_nonfinite_gradients_as_torch(dev):
         oa.step()
     with pytest.raises(ValueError):
         HipAdam(pa, clip=-1.0)
+
+
+@pytest.mark.parametrize("mlp", ["x3", "torch"])
+def test_bench_shape_step_matches_reference(dev, mlp):
+    """The bench's own C3 shape (BASELINE configs[2], bench.py bench_train): 1024
+    pixels scattered over the lego test views, perturb 1, training-mode u, the
+    trained lego checkpoint, MSE coarse + fine (trainers/nerf.py:39-76) against
+    a random target; tests/golden/t3_c3_scatter.npz + tg_t3_c3_scatter.npz
+    (make_train_fullgrad.py t3: the reference's per-chunk methods on one
+    1024-ray chunk, VR:154-193, and its self-distance under 16 exact
+    reparametrisations). The rays the bench builds (camera_rays_at) agree with
+    the reference's (VR:115-143); the step runs on the reference's own rays and
+    draws; every gradient tensor within 2x the reference's own distance from
+    itself (full loss and coarse loss alone)."""
+    from nerfhip.train import NerfTrainer, camera_rays_at
+    z = load("t3_c3_scatter")
+    ck = torch.load(os.path.join(REPO, "checkpoints", "lego", "latest.pth"), map_location="cpu",
+                    weights_only=True)["net"]
+    tr = NerfTrainer(dev, {k: v.float() for k, v in ck.items()}, mlp=mlp)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
+    ro_b, rd_b = camera_rays_at(t(cams["poses"].astype(np.float32)), t(z["K"]),
+                                t(z["pix"].astype(np.int64)), t(z["view"].astype(np.int64)), 800)
+    assert float((ro_b - t(z["rays_o"])).abs().max()) == 0.0
+    assert float((rd_b - t(z["rays_d"])).abs().max()) <= 2e-7
+    ro, rd = t(z["rays_o"]), t(z["rays_d"])
+    out = tr.forward(ro, rd, t(z["t_rand"]), t(z["u"]))
+    assert max_err(out["rgb_map_0"].detach().cpu().numpy(), z["rgb_map_0"]) < 1e-5
+    assert psnr(out["rgb_map"].detach().cpu().numpy(), z["rgb_map"]) > 60.0
+    losses = tr.loss(out, t(z["target"]))
+    assert abs(losses["loss_coarse"].item() - float(z["loss_coarse"])) <= 1e-6 * float(z["loss_coarse"])
+    assert abs(losses["loss"].item() - float(z["loss"])) <= 1e-4 * float(z["loss"])
+    tr.opt.zero_grad(set_to_none=True)
+    losses["loss_coarse"].backward(retain_graph=True)
+    _elementwise_grads("t3_c3_scatter", {k: p.grad for k, p in tr.named_parameters()},
+                       coarse=True)
+    tr.opt.zero_grad(set_to_none=True)
+    losses["loss"].backward()
+    _elementwise_grads("t3_c3_scatter", {k: p.grad for k, p in tr.named_parameters()})
