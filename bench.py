@@ -299,6 +299,37 @@ def main():
                 p4, "r2_c4_frame16", H, W, ckpt)
             del p4
         result["c4_ess_ert"] = rec
+    if args.config == "c2" and not args.no_c4 and not args.no_perturb:
+        # lego.yaml's own eval configuration (run.py --type evaluate): ESS + ERT
+        # at 0.01 (lego.yaml:96-99) AND perturb 1 (:22): per-ray jittered depths
+        # after the ESS fold (VR:1080-1085)
+        torch.cuda.empty_cache()
+        y_steps = max(1, min(args.steps, 5))
+        py, ely, roofy = measure(args.precision, True, y_steps, 1, perturb=True)
+        raysy = H * W * y_steps
+        rec = {"metric": "Mrays/s + ms/frame, lego 800x800 (64c+128f), lego.yaml eval: ESS + "
+                         "ERT + perturb 1",
+               "value": raysy / ely / 1e6, "unit": "Mrays/s", "steps": y_steps, "warmup": 1,
+               "ms_per_step": ely / y_steps * 1e3, "dtype": DTYPES[args.precision],
+               "config": {"workload": "lego 800x800, 64c+128f, ESS + ERT (threshold 0.01, "
+                                      "occupancy grid sphere 1.2 | 10 % noise as the Renderer "
+                                      "draws it, self-updated by the reference's rule), perturb "
+                                      "1 (one [H*W, 64] draw per frame), eval, 1 frame per step "
+                                      "(test poses cycled)",
+                          "baseline_config": "configs[3] as run.py --type evaluate renders it "
+                                             "(lego.yaml)",
+                          "parallelism": f"2048-ray chunks round-robin x{world} + RCCL "
+                                         f"all-gather"},
+               "roofline": {k: roofy[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
+                                                  "avg_launch_ms", "launches")},
+               "ert_compaction": ert_report(py, raysy, world, args.ert_segment, dev)}
+        del py
+        if rank == 0 and world == 1:
+            py = make_pipe(args.precision, True)
+            rec["parity_vs_reference_frame"] = reference_frame_parity(
+                py, "r3_c4_yaml_frame24", H, W, ckpt)
+            del py
+        result["lego_yaml_eval"] = rec
     if args.config == "c2" and not args.no_perturb:
         # what `run.py --type evaluate` with lego.yaml runs: perturb 1 at eval
         # (lego.yaml:22, VR:228-235), per-ray jittered coarse depths
@@ -342,8 +373,10 @@ def make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb=False):
     SURVEY §8e), grid self-updates replayed. perturb: the reference's eval-mode
     stratified jitter (perturb 1, lego.yaml:22; VR:228-235), one [n, 64] uniform
     draw per band on the device (torch's Philox) inside the frame, so the coarse
-    pass reads per-ray depth rows. tests/test_gpu_dist.py drives this same
-    function from two processes."""
+    pass reads per-ray depth rows; with ESS + ERT (lego.yaml's own eval
+    configuration) one [H * W, 64] draw per frame from a per-frame seed, the same
+    on every rank, each chunk reading its rows. tests/test_gpu_dist.py drives
+    this same function from two processes."""
     from nerfhip.dist import render_frame_interleaved, render_frame_sharded
     import torch
 
@@ -357,10 +390,18 @@ def make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb=False):
             return pipe.render_image(H, W, pose, K, t_rand=tr, p0=p0, n=n)
         return render
 
+    count = [0]
+
     def frame(pose, K):
         if ess_ert:
+            tr = None
+            if perturb:   # the frame's draws, the same on every rank (seeded per frame)
+                g = torch.Generator(device=dev).manual_seed(7000 + count[0])
+                tr = torch.rand((H * W, pipe.N_samples), device=dev, generator=g)
+            count[0] += 1
             return render_frame_interleaved(
-                lambda cs: pipe.render_chunks(H, W, pose, K, cs), H, W, rank, world, dev)
+                lambda cs: pipe.render_chunks(H, W, pose, K, cs, t_rand=tr), H, W, rank, world,
+                dev)
         return render_frame_sharded(band(pose, K), H, W, rank, world, dev)
     return frame
 
@@ -809,13 +850,26 @@ def reference_frame_parity(pipe, name, H, W, ckpt):
     with open(resolve(ckpt), "rb") as f:
         if hashlib.sha256(f.read()).hexdigest() != str(z["ckpt_sha256"]):
             return {"skipped": "checkpoint differs from the one the reference frame used"}
+    own = bool(z["grid_own"]) if "grid_own" in z else False
+    gen = torch.Generator().manual_seed(int(z["seed"])) if int(z["perturb"]) else None
     if bool(z["ess"]):
-        from nerfhip.synthetic import make_occupancy_grid
-        gs = z["grid_spec"]
-        pipe.set_grid(make_occupancy_grid(int(gs[0]), int(gs[1]), float(gs[2]), float(gs[3])))
+        if own:   # the Renderer's own grid (VR:857-864), the generator's first draw
+            torch.rand((128, 128, 128), generator=gen)
+            bits = np.unpackbits(z["grid_init_bits"])[:128 ** 3].astype(bool)
+            pipe.set_grid(bits.reshape(128, 128, 128))
+        else:
+            from nerfhip.synthetic import make_occupancy_grid
+            gs = z["grid_spec"]
+            pipe.set_grid(make_occupancy_grid(int(gs[0]), int(gs[1]), float(gs[2]),
+                                              float(gs[3])))
         pipe.grid_update_counter = int(z["counter0"])
+    t_rand = None
+    if gen is not None:   # the reference's per-chunk perturb draws (VR:233, :1083)
+        t_rand = torch.cat([torch.rand((min(2048, H * W - c), 64), generator=gen)
+                            for c in range(0, H * W, 2048)]).to(pipe.device)
     pipe.ert_stats = []
-    g = {k: v.cpu().numpy() for k, v in pipe.render_image(H, W, z["pose"], z["K"]).items()}
+    g = {k: v.cpu().numpy() for k, v in
+         pipe.render_image(H, W, z["pose"], z["K"], t_rand=t_rand).items()}
     torch.cuda.synchronize()
     n = H * W
     gt = composite_white(decode_png(z["gt_png"]))

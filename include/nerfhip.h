@@ -38,8 +38,9 @@ enum {
 const char* nerf_last_error(void);
 /* ABI version, bumped on every change of a struct layout or signature below
  * (2: NerfWgradDesc amax_a2/amax_b2/ldo, NerfX3BwdIO d_raw_t, the
- * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4) */
-#define NERF_ABI_VERSION 2
+ * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4; 3: NerfWgradDesc
+ * bsa / bsb, the block-layout operands of round 5) */
+#define NERF_ABI_VERSION 3
 int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
  * source tree this library was compiled from (nerfhip/_lib.py refuses a
@@ -248,6 +249,11 @@ typedef struct NerfWgradDesc {
   int64_t ldo;            /* row stride of the partials ([M][ldo] at part + z * ldpart);
                              0: N. Two descriptors with the same A can write the column
                              blocks of one gradient (the skip layer's [enc | h4]) */
+  int64_t bsa, bsb;       /* sample-block strides of A / B in floats (ABI 3): element (r, p)
+                             of an operand is at r * ld + (p / 16) * bs + p % 16. 0 (or 16):
+                             feature-major rows ([M][ld], ld >= P); 16 * rows with ld = 16:
+                             the 16-sample block layout [P / 16][rows][16] of the fused
+                             training kernels (nerf_mlp_train_forward_x3) */
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
 /* The same with a K split per output tile: tile_chunks[t] (1 .. zmax, < 256)

@@ -1684,7 +1684,7 @@ __device__ __forceinline__ void wgrad_dma_body(
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
     const float amax_b, float* __restrict__ part, int64_t ldpart,
     float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z,
-    int64_t ldo) {
+    int64_t ldo, int64_t bsa, int64_t bsb) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
@@ -1695,28 +1695,39 @@ __device__ __forceinline__ void wgrad_dma_body(
   const int ea = act_exponent(amax_a), eb = act_exponent(amax_b);
   const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
 
-  // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1)
-  const int nbA = (int)((int64_t)M * lda * 4), nbB = (int)((int64_t)N * ldb * 4);
+  // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1).
+  // Element (r, p) of an operand: r * ld + (p >> 4) * bs + (p & 15) (bs 16:
+  // feature-major rows; 16 * rows with ld 16: the 16-sample block layout). A K
+  // step's block offset rides in soffset, the lane's row and column in voffset;
+  // num_records = the operand's extent (rows past M / N read 0)
+  const int nbA = (int)((((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16) * 4);
+  const int nbB = (int)((((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16) * 4);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nbA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
   unsigned voA[4], voB[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = 4 * wave + i, t = q >> 1, h = q & 1;
-    const int col = 8 * (lane >> 4) + 4 * h;
+    const int col = 8 * (lane >> 4) + 4 * h;     // sample of the K step, 0 .. 31
     const int ra = m0 + 16 * t + (lane & 15), rb = n0 + 16 * t + (lane & 15);
-    voA[i] = ra < M ? (unsigned)(((int64_t)ra * lda + col) * 4) : (unsigned)nbA;
-    voB[i] = rb < N ? (unsigned)(((int64_t)rb * ldb + col) * 4) : (unsigned)nbB;
+    voA[i] = ra < M ? (unsigned)(((int64_t)ra * lda + (col >> 4) * bsa + (col & 15)) * 4)
+                    : (unsigned)nbA;
+    voB[i] = rb < N ? (unsigned)(((int64_t)rb * ldb + (col >> 4) * bsb + (col & 15)) * 4)
+                    : (unsigned)nbB;
   }
   // piece I of granule g: A (g even) or B (g odd) of step g >> 1, into slot g % 5
   auto issue_piece = [&](int g, auto Ic) {
     constexpr int I = decltype(Ic)::value;
     if (g >= ngran) return;
-    const int64_t p0 = pb + (int64_t)(g >> 1) * kstride;
-    const int so = __builtin_amdgcn_readfirstlane((int)(p0 * 4));
+    const int64_t p0 = pb + (int64_t)(g >> 1) * kstride;   // a multiple of 32
     uint4* dst = &ring[g % kWgRing][(4 * wave + I) * 64];
-    if (g & 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_ptr_t)dst, 16, (int)voB[I], so, 0, 0);
-    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)dst, 16, (int)voA[I], so, 0, 0);
+    if (g & 1) {
+      const int so = __builtin_amdgcn_readfirstlane((int)((p0 >> 4) * bsb * 4));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_ptr_t)dst, 16, (int)voB[I], so, 0, 0);
+    } else {
+      const int so = __builtin_amdgcn_readfirstlane((int)((p0 >> 4) * bsa * 4));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_ptr_t)dst, 16, (int)voA[I], so, 0, 0);
+    }
   };
   auto issue = [&](int g) {
     issue_piece(g, std::integral_constant<int, 0>{});
@@ -1853,7 +1864,7 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
     float* __restrict__ part, float* __restrict__ bias_part) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
   wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, *amax_a, *amax_b, part, (int64_t)M * N, bias_part,
-                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, N);
+                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, N, 16, 16);
 }
 
 // Several weight gradients in one launch (the whole backward of a network):
@@ -1887,7 +1898,8 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
   const float mb = d.amax_b2 ? fmaxf(*d.amax_b, *d.amax_b2) : *d.amax_b;
   const int64_t ldo = d.ldo ? d.ldo : d.N;
   wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, ma, mb, d.part,
-                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z, ldo);
+                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z, ldo, d.bsa ? d.bsa : 16,
+                 d.bsb ? d.bsb : 16);
   if (z != 0 || Z >= bt.Zmax) return;
   // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)
   const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
@@ -2257,10 +2269,12 @@ extern "C" int nerf_x3_layer_ex(const float* w_packed, const int* w_scale, int m
 }
 
 static bool wgrad_dma_ok(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
-                         int64_t P) {
-  return P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+                         int64_t P, int64_t bsa = 16, int64_t bsb = 16) {
+  const int64_t ea = ((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16;   // operand extents
+  const int64_t eb = ((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16;
+  return P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 && bsa % 4 == 0 && bsb % 4 == 0 &&
          ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
-         (int64_t)M * lda * 4 < ((int64_t)1 << 31) && (int64_t)N * ldb * 4 < ((int64_t)1 << 31);
+         ea * 4 < ((int64_t)1 << 31) && eb * 4 < ((int64_t)1 << 31);
 }
 
 extern "C" int nerf_x3_wgrad(const float* A, int64_t lda, int M, const float* B, int64_t ldb,
@@ -2295,12 +2309,16 @@ extern "C" int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const in
   for (int k = 0; k < n; ++k) {
     const NerfWgradDesc& d = descs[k];
     const int64_t ldo = d.ldo ? d.ldo : d.N;
+    const int64_t bsa = d.bsa ? d.bsa : 16, bsb = d.bsb ? d.bsb : 16;
+    // feature-major rows hold every sample (ld >= P); in the block layout a
+    // block holds every row (bs >= 16 rows, ld = 16)
     NERF_REQUIRE(d.A && d.B && d.amax_a && d.amax_b && d.part && d.M > 0 && d.N > 0 &&
-                     d.P >= 0 && d.lda >= d.P && d.ldb >= d.P && ldo >= d.N &&
+                     d.P >= 0 && (bsa == 16 ? d.lda >= d.P : d.lda == 16 && bsa >= 16 * d.M) &&
+                     (bsb == 16 ? d.ldb >= d.P : d.ldb == 16 && bsb >= 16 * d.N) && ldo >= d.N &&
                      d.ldpart >= (int64_t)(d.M - 1) * ldo + d.N &&
                      (!d.bias_part || d.ldbias >= d.M),
                  "nerf_x3_wgrad_batch: bad descriptor");
-    NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P),
+    NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, bsa, bsb),
                  "nerf_x3_wgrad_batch: operands must be aligned (P % 32 == 0, 16-B rows, < 2 GiB)");
     bt.d[k] = d;
     const int mt = (int)cdiv(d.M, kWgTile), ntl = (int)cdiv(d.N, kWgTile);

@@ -432,7 +432,7 @@ class NerfPipeline:
         return [c for c in range(total)
                 if any((cf + per * c + k) % self.grid_update_interval == 0 for k in range(per))]
 
-    def render_chunks(self, H, W, pose, K, chunks):
+    def render_chunks(self, H, W, pose, K, chunks, t_rand=None):
         """The reference chunks `chunks` (ascending ids of 2048 consecutive
         pixels, VR:147) of a frame whose other chunks other ranks render
         concurrently (dist.render_frame_interleaved: chunk c on rank c mod P),
@@ -450,7 +450,8 @@ class NerfPipeline:
         order, and the updates after the last owned chunk are replayed too,
         so every rank leaves the frame with the sequential loop's grid and
         counter. Cost: one extra chunk per foreign update chunk (2 per 500
-        ERT calls)."""
+        ERT calls). t_rand: the frame's perturb draws [H * W, N_samples] (every
+        rank holds the same; a chunk reads its own rows)."""
         total = -(-H * W // REF_CHUNK)
         chunks = [int(c) for c in chunks]
         if chunks != sorted(set(chunks)) or (chunks and not 0 <= chunks[0] <= chunks[-1] < total):
@@ -466,15 +467,16 @@ class NerfPipeline:
         def rows(cs):
             idx = torch.cat([torch.arange(c * REF_CHUNK, c * REF_CHUNK + min(
                 REF_CHUNK, H * W - c * REF_CHUNK), device=self.device) for c in cs])
-            return rays_o.index_select(0, idx), rays_d.index_select(0, idx)
+            tr = None if t_rand is None else t_rand.index_select(0, idx)
+            return rays_o.index_select(0, idx), rays_d.index_select(0, idx), tr
 
         def block(i0, i1):           # own chunks chunks[i0:i1] as one block, no updates inside
             if i1 <= i0:
                 return
-            ro, rd = rows(chunks[i0:i1])
+            ro, rd, tr = rows(chunks[i0:i1])
             self._updates_on = False
             try:
-                self.render_rays(ro, rd, outputs=outputs, off=offs[i0])
+                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i0])
             finally:
                 self._updates_on = True
 
@@ -491,12 +493,12 @@ class NerfPipeline:
             block(i, j)
             i = j
             self.grid_update_counter = cf + per * u
-            ro, rd = rows([u])
+            ro, rd, tr = rows([u])
             if i < len(chunks) and chunks[i] == u:
-                self.render_rays(ro, rd, outputs=outputs, off=offs[i])
+                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i])
                 i += 1
             else:
-                self._replay(lambda: self.render_rays(ro, rd))
+                self._replay(lambda: self.render_rays(ro, rd, t_rand=tr))
         block(i, len(chunks))
         self.grid_update_counter = cf + per * total
         return maps_dict(outputs) if chunks else {}

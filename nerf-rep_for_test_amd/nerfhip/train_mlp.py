@@ -528,7 +528,7 @@ class _WgradDesc(ctypes.Structure):
                 ("ldpart", ctypes.c_int64), ("bias_part", ctypes.c_void_p),
                 ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int),
                 ("amax_a2", ctypes.c_void_p), ("amax_b2", ctypes.c_void_p),
-                ("ldo", ctypes.c_int64)]
+                ("ldo", ctypes.c_int64), ("bsa", ctypes.c_int64), ("bsb", ctypes.c_int64)]
 
 
 _NCU = {}
@@ -542,7 +542,67 @@ def _n_cu(device):
 
 
 def _dma_ok(t):
+    if isinstance(t, BlockRows):
+        return t.data_ptr() % 16 == 0
     return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
+BLOCK = 16   # samples per block of the block layout
+
+
+class BlockRows:
+    """Rows r0 .. r0 + M of a [R, P] activation stored in the 16-sample block
+    layout: buf is [nb, R, 16] (nb = ceil(P / 128) * 8 blocks: whole 128-sample
+    tiles), element (r, p) at buf[p // 16, r0 + r, p % 16]. A wave of the fused
+    training kernels owns 16 samples, so every row it writes is one contiguous
+    64-B run and a (wave, layer) output one contiguous 16 KiB region; a K step
+    of the weight gradients (32 samples) reads two contiguous regions per
+    operand instead of one 128-B run per row (NerfWgradDesc bsa / bsb)."""
+
+    def __init__(self, buf, r0, M, P):
+        assert buf.dim() == 3 and buf.shape[2] == BLOCK and buf.is_contiguous()
+        assert 0 <= r0 and r0 + M <= buf.shape[1] and buf.shape[0] * BLOCK >= P
+        self.buf, self.r0, self.M, self.P = buf, int(r0), int(M), int(P)
+        self.shape = (self.M, self.P)
+        self.device = buf.device
+
+    @staticmethod
+    def alloc(R, P, dev):
+        nb = -(-P // 128) * (128 // BLOCK)
+        return BlockRows(torch.empty((nb, R, BLOCK), device=dev, dtype=torch.float32), 0, R, P)
+
+    def rows(self, a, b):
+        """Rows a .. b of this operand (a view)."""
+        return BlockRows(self.buf, self.r0 + a, b - a, self.P)
+
+    def data_ptr(self):
+        return self.buf.data_ptr() + 4 * BLOCK * self.r0
+
+    def numel(self):   # the whole buffer: the operand's extent lies inside it
+        return self.buf.numel()
+
+    def stride(self, dim):   # NerfWgradDesc lda (the row stride) and bs
+        return BLOCK if dim == 0 else 1
+
+    @property
+    def block_stride(self):
+        return BLOCK * self.buf.shape[1]
+
+    def dense(self):
+        """The same rows feature-major, [M, P] (tests, the fallback paths)."""
+        b = self.buf[:, self.r0:self.r0 + self.M, :]
+        return b.permute(1, 0, 2).reshape(self.M, -1)[:, :self.P]
+
+    @staticmethod
+    def from_dense(A, R=None):
+        """A [M, P] copied into a new block-layout buffer (tests, tools)."""
+        M, P = A.shape
+        out = BlockRows.alloc(R or M, P, A.device)
+        nb = out.buf.shape[0]
+        full = torch.zeros((M, nb * BLOCK), device=A.device, dtype=torch.float32)
+        full[:, :P] = A
+        out.buf[:, :M, :] = full.view(M, nb, BLOCK).permute(1, 0, 2)
+        return out.rows(0, M)
 
 
 WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "512"))
@@ -598,9 +658,9 @@ class WgradBatch:
         same A; no result of its own). One contiguous gradient from operands in
         two buffers (the skip layer's [encoding | h4])."""
         if amax_a is None:
-            amax_a = _absmax(A)
+            amax_a = _absmax(A.dense() if isinstance(A, BlockRows) else A)
         if amax_b is None:
-            amax_b = _absmax(B)
+            amax_b = _absmax(B.dense() if isinstance(B, BlockRows) else B)
         self.req.append((A, B, amax_a, amax_b, with_bias, width, into))
         return len(self.req) - 1
 
@@ -609,13 +669,16 @@ class WgradBatch:
         if not req:
             return []
         P = req[0][0].shape[1]
+        blocked = any(isinstance(t, BlockRows) for r in req for t in r[:2])
         ok = (len(req) <= 16 and P % 32 == 0 and
               all(A.shape[1] == P and B.shape[1] == P and _dma_ok(A) and _dma_ok(B)
                   and A.numel() * 4 < (1 << 31) and B.numel() * 4 < (1 << 31)
                   for A, B, *_ in req))
         if not ok:
             one = lambda m: torch.maximum(*m) if isinstance(m, tuple) else m   # noqa: E731
-            res = [_wgrad(A, B, one(aa), one(ab), wb) for A, B, aa, ab, wb, _, _ in req]
+            dn = lambda t: t.dense() if isinstance(t, BlockRows) else t   # noqa: E731
+            assert not blocked or P % 32 != 0, "block-layout operands the batch cannot take"
+            res = [_wgrad(dn(A), dn(B), one(aa), one(ab), wb) for A, B, aa, ab, wb, _, _ in req]
             for k, (A, B, _, _, wb, width, into) in enumerate(req):
                 if into is not None:   # the column blocks joined on the host
                     s, c0 = into
@@ -652,10 +715,11 @@ class WgradBatch:
             (a1, a2), (b1, b2) = two(aa), two(ab)
             off, wdt = region[into[0]] if into is not None else region[k]
             off += into[1] if into is not None else 0
+            bs = lambda t: t.block_stride if isinstance(t, BlockRows) else 0   # noqa: E731
             descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
                                   a1, b1, part.data_ptr() + 4 * off, ldt,
                                   part.data_ptr() + 4 * (ld + boff) if wb else None, ldt,
-                                  A.shape[0], B.shape[0], a2, b2, wdt)
+                                  A.shape[0], B.shape[0], a2, b2, wdt, bs(A), bs(B))
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
         zarr = (ctypes.c_int * len(zs))(*zs)

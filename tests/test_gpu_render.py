@@ -496,9 +496,11 @@ def _band_frame(dev, H, W, world, counter0, grid, params, prec="f16x3"):
     return nd.unpack_maps(full, H, W, set(nd.MAP_ORDER)), states, (pose, K)
 
 
-def _interleaved_frame(dev, H, W, world, counter0, grid, params, pose, K, prec="f16x3"):
+def _interleaved_frame(dev, H, W, world, counter0, grid, params, pose, K, prec="f16x3",
+                       t_rand=None):
     """render_frame_interleaved's chunk-set / pack / index_select path with the
-    world ranks rendered one after another on one device (same start state)."""
+    world ranks rendered one after another on one device (same start state);
+    t_rand: the frame's perturb draws, every rank reading its chunks' rows."""
     from nerfhip import dist as nd
     tiles, states, evals = [], [], []
     for r in range(world):
@@ -508,7 +510,7 @@ def _interleaved_frame(dev, H, W, world, counter0, grid, params, pose, K, prec="
         pipe.set_grid(grid)
         pipe.grid_update_counter = counter0
         mine, n, n_pad = nd.chunk_set(H, W, r, world)
-        maps = pipe.render_chunks(H, W, pose, K, mine)
+        maps = pipe.render_chunks(H, W, pose, K, mine, t_rand=t_rand)
         tiles.append(nd.pack_maps(maps, n, n_pad, dev))
         states.append((pipe.grid.clone(), pipe.grid_update_counter))
         evals.append(pipe.evaluated_samples())
@@ -640,3 +642,36 @@ def test_sample_fine_shared_u(dev, S, NI, kind):
     ref = np.sort(np.concatenate([zc, O.sample_fine(mids, wc[:, 1:-1],
                                                    np.broadcast_to(u, (n, NI)))], -1), -1)
     assert np.array_equal(zall.cpu().numpy(), ref)
+
+
+def test_interleaved_perturbed_ess_ert_equals_one_pass(dev):
+    """lego.yaml's eval configuration sharded (ESS + ERT + perturb 1, bench
+    lego_yaml_eval): chunks dealt round-robin to 2 / 3 / 8 ranks, each reading its
+    chunks' rows of the frame's perturb draws, with a grid self-update inside
+    the frame: bit-exactly the one-pass perturbed frame, grid and counter."""
+    from nerfhip.synthetic import make_occupancy_grid, make_params
+    H = W = 96
+    params = make_params(0, 3.0, 1.0)
+    grid = make_occupancy_grid(4, 128, 0.5, 0.01)
+    cams = load("lego_test_cameras")
+    f = 0.5 * 800 / np.tan(0.5 * float(cams["camera_angle_x"]))
+    K = np.array([[f, 0, 400 - 352], [0, f, 400 - 352], [0, 0, 1]], np.float32)
+    pose = cams["poses"][0]
+    tr = torch.rand((H * W, 64), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    one = _pipe(dev, N_samples=64, N_importance=128, enable_ess=True, enable_ert=True,
+                ert_threshold=0.01)
+    one.set_weights(params)
+    one.set_grid(grid)
+    one.grid_update_counter = 496
+    direct = one.render_image(H, W, pose, K, t_rand=tr)
+    plain = _interleaved_frame(dev, H, W, 1, 496, grid, params, pose, K)[0]
+    assert not torch.equal(plain["rgb_map"].reshape(-1), direct["rgb_map"].reshape(-1))
+    for world in (1, 2, 3, 8):
+        got, states, _ = _interleaved_frame(dev, H, W, world, 496, grid, params, pose, K,
+                                            t_rand=tr)
+        for k in direct:
+            assert torch.equal(torch.nan_to_num(got[k].reshape(-1), 7.0),
+                               torch.nan_to_num(direct[k].reshape(-1), 7.0)), (world, k)
+        for g, c in states:
+            assert c == one.grid_update_counter
+            assert torch.equal(g, one.grid)
