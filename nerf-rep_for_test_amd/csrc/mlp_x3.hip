@@ -1679,6 +1679,9 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 // subset z's partials go to part + z * ldpart ([M][N]) and bias_part + z *
 // ldbias ([M]).
 constexpr int kWgRing = 5;
+#ifndef NERF_WGRAD_ABL
+#define NERF_WGRAD_ABL 0
+#endif
 __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
@@ -1719,6 +1722,9 @@ __device__ __forceinline__ void wgrad_dma_body(
   auto issue_piece = [&](int g, auto Ic) {
     constexpr int I = decltype(Ic)::value;
     if (g >= ngran) return;
+#if NERF_WGRAD_ABL == 2   // timing-only ablation: no operand stream (stale LDS)
+    return;
+#endif
     const int64_t p0 = pb + (int64_t)(g >> 1) * kstride;   // a multiple of 32
     uint4* dst = &ring[g % kWgRing][(4 * wave + I) * 64];
     if (g & 1) {
@@ -1818,9 +1824,13 @@ __device__ __forceinline__ void wgrad_dma_body(
           ah[i] = op_hi(v);
           al[i] = op_lo(v);
         }
+#if NERF_WGRAD_ABL == 1   // timing-only ablation: no MFMAs (operands kept live)
+        asm volatile("" ::"v"(ah[i]), "v"(al[i]), "v"(bh), "v"(bl));
+#else
         acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
         acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
         acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
+#endif
       }
     };
     tile(std::integral_constant<int, 0>{});

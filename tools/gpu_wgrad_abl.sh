@@ -1,13 +1,12 @@
 #!/bin/bash
-# timing-only ablations of the weight-gradient kernel (libraries built from
-# temporary patches: 1 = no MFMAs, 2 = no LDS-DMA issue, 3 = no FP16 split)
+# timing-only ablations of the batched weight-gradient kernel (make variant V=wabl1/2):
+# 1 = no MFMAs, 2 = no operand stream; the shipped kernel in between
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-mkdir -p gpurun_out/wabl
-for v in base abl1 abl2 abl3; do
-  if [ $v = base ]; then unset NERFHIP_LIB; else export NERFHIP_LIB=$PWD/nerf-rep_for_test_amd/lib/libnerfhip_$v.so; fi
-  echo "== $v"
-  timeout -k 10 200 python tools/train_kernels_bench.py > gpurun_out/wabl/$v.log 2>&1 || exit $?
-  grep "wgrad" gpurun_out/wabl/$v.log
+O=gpurun_out/${TAG:-wabl}
+mkdir -p $O
+for v in base wabl1 wabl2 base; do
+  if [ $v = base ]; then L=""; else L="NERFHIP_LIB=nerf-rep_for_test_amd/lib/libnerfhip_$v.so"; fi
+  env $L timeout -k 10 120 python tools/wgrad_layout_bench.py > $O/$v.log 2>&1 || { cat $O/$v.log; exit 1; }
+  echo "== $v"; grep -E "us" $O/$v.log
 done
