@@ -39,7 +39,8 @@ const char* nerf_last_error(void);
 /* ABI version, bumped on every change of a struct layout or signature below
  * (2: NerfWgradDesc amax_a2/amax_b2/ldo, NerfX3BwdIO d_raw_t, the
  * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4; 3: NerfWgradDesc
- * bsa / bsb, the block-layout operands of round 5) */
+ * bsa / bsb, NerfX3TrainOut.bs / NerfX3BwdIO.bs and the encoding-backward layout
+ * arguments: the T16 activation layout of round 5) */
 #define NERF_ABI_VERSION 3
 int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
@@ -286,6 +287,11 @@ typedef struct NerfX3TrainOut {
   unsigned short* bits[9];
   float* amax;
   int64_t ld;
+  int64_t bs;   /* 0: feature-major rows (row stride ld >= P); > 0 (a multiple of 256):
+                   the T16 layout, block stride bs floats, every act[] a row of one
+                   [ceil(P/128) * 8][rows][16] buffer starting on a 16-row group:
+                   row 16 t + 4 g + r of sample 16 b + s at b * bs + t * 256 + r * 64 +
+                   g * 16 + s (ABI 3; nerfhip.train_mlp.BlockRows) */
 } NerfX3TrainOut;
 int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_head, const float* pts,
                               const float* dirs, const float* zero, int64_t P,
@@ -319,6 +325,7 @@ typedef struct NerfX3BwdIO {
   float* dmax;
   int64_t ld;
   float* d_raw_t;   /* nullable: d raw feature-major, rows (stride ld) d sigma, d r, d g, d b */
+  int64_t bs;       /* as NerfX3TrainOut.bs (ABI 3) */
 } NerfX3BwdIO;
 /* nerf_mlp_forward_x3_clock: nerf_mlp_forward_x3's computation (same outputs)
  *   by a diagnostic twin of its kernel that stamps (s_memtime, s_memrealtime)
@@ -351,18 +358,22 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
  *   feature-major [3 + 6 * n_freq][ldd]. */
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream);
-/* The same on d_enc + d_enc2 (elementwise, same row stride; d_enc2
- * nullable): the encoding's two consumers' gradients summed in the kernel.
- * enc (nullable): the forward's encoding rows (nerf_freq_encode_fm's layout,
- * stride ldd), whose sin / cos values are read instead of recomputed. */
+/* The same on d_enc + d_enc2 (elementwise, same layout; d_enc2 nullable): the
+ * encoding's two consumers' gradients summed in the kernel. enc (nullable):
+ * the forward's encoding rows, whose sin / cos values are read instead of
+ * recomputed. Layouts (ABI 3): d_enc / d_enc2 (ldd, bsd), enc (lde, bse); bs 0 =
+ * feature-major rows of stride ld (>= P), bs > 0 = the T16 layout of
+ * NerfX3TrainOut.bs. */
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                     const float* enc, const float* x, int64_t ldx, int64_t P,
-                                     int n_freq, float* dx, nerf_stream_t stream);
+                                     int64_t bsd, const float* enc, int64_t lde, int64_t bse,
+                                     const float* x, int64_t ldx, int64_t P, int n_freq,
+                                     float* dx, nerf_stream_t stream);
 /* ... taken on to the sample depths of nerf_mlp_train_forward_x3_rays: dz[p] =
  * sum_c dx[p][c] * rays_d[p / S][c] (enc required). */
 int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                    const float* enc, const float* rays_d, int S, int64_t P,
-                                    int n_freq, float* dz, nerf_stream_t stream);
+                                    int64_t bsd, const float* enc, int64_t lde, int64_t bse,
+                                    const float* rays_d, int S, int64_t P, int n_freq, float* dz,
+                                    nerf_stream_t stream);
 /* nerf_x3_pack: packs n weight matrices for the x3 training kernels in one
  * launch set. descs (device) = n records {const float* src; int64_t ldr, ldc;
  * const int* rowmap; const int* colmap; int M, K; void* out; int* sw;

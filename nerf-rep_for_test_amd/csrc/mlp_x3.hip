@@ -359,30 +359,73 @@ __device__ __forceinline__ void lds_max_u32(unsigned* p, unsigned v) {
 #define NERF_ACT_STORE_AUX 2
 #endif
 
+// Where element (row, sample p) of a training activation / gradient buffer
+// lives, in floats from the output's pointer (rows start on 16-row groups).
+// bs == 0: feature-major rows [rows][ld], element row * ld + p. bs > 0: the
+// 16-sample tile layout T16 -- a block of 16 samples holds every row of the
+// buffer (block stride bs floats), and inside it each 16-row group is one
+// 1-KiB tile with row 16 t + 4 g + r of sample s at t * 256 + r * 64 + g * 16 + s.
+// Element r of a 16 x 16 MFMA accumulator tile (lane 16 g + s holds rows 4 g ..
+// 4 g + 3 of sample s) is then 256 contiguous bytes for the whole wave: one
+// store instruction writes whole lines, and a K step of the weight gradients
+// (32 samples) reads two contiguous 16-KiB runs per 256-row operand
+// (NerfWgradDesc bsa / bsb; nerfhip.train_mlp.BlockRows).
+struct Lay {
+  int64_t ld, bs;
+  int64_t nblk;   // T16: the buffer's 16-sample blocks (whole 128-sample tiles)
+  __device__ __forceinline__ static int rowpart(int row) {   // T16, floats
+    return (row >> 4) * 256 + (row & 3) * 64 + ((row >> 2) & 3) * 16;
+  }
+  // element (row, p), bytes
+  __device__ __forceinline__ unsigned elem(int row, int64_t p) const {
+    return bs ? (unsigned)(((p >> 4) * bs + rowpart(row) + (p & 15)) * 4)
+              : (unsigned)(((int64_t)row * ld + p) * 4);
+  }
+  // bytes an output of `rows` rows spans from its pointer (its num_records)
+  __device__ __forceinline__ int extent(int rows) const {
+    return bs ? (int)(((nblk - 1) * bs + ((rows + 15) & ~15) * 16) * 4) : (int)((int64_t)rows * ld * 4);
+  }
+};
+
 struct ActStore {
-  __amdgpu_buffer_rsrc_t rs;   // the layer's output rows (num_records: rows * ld * 4)
+  __amdgpu_buffer_rsrc_t rs;   // the layer's output rows (num_records: Lay::extent)
   __amdgpu_buffer_rsrc_t rb;   // its ReLU-bit words (num_records 0: no bits)
-  unsigned soff;               // uniform: the tile's first sample of this wave, * 4
+  unsigned soff;               // uniform: this (tile, wave)'s first sample / block, bytes
   unsigned sboff;              // uniform: this (tile, wave)'s first bit word, * 2
-  unsigned ld4;                // uniform: row stride in bytes
+  unsigned c4, ts, rstr;       // uniform, bytes: per lane group g4 (rows 4 g4 ..), per
+                               // 16-row tile, per row r of a lane's 4 (Lay; set by set_lay)
   unsigned wb;                 // bits of the current 4-tile block
   bool bits, valid;
   bool on = true;              // uniform: false = these rows are not stored (null output)
+  __device__ __forceinline__ void set_lay(const Lay& L, int64_t tile, int wave) {
+    if (L.bs) {
+      soff = (unsigned)((tile * 8 + wave) * L.bs * 4);
+      c4 = 64u; ts = 1024u; rstr = 256u;
+    } else {
+      soff = (unsigned)((tile * kX3Tile + wave * 16) * 4);
+      c4 = (unsigned)(L.ld * 16); ts = (unsigned)(L.ld * 64); rstr = (unsigned)(L.ld * 4);
+    }
+  }
+  // this lane's offset of its rows 4 g4 + r of tile t: lane_off() + t * ts + r * rstr
+  __device__ __forceinline__ unsigned lane_off() const {
+    unsigned lid = __lane_id();
+    asm volatile("" : "+v"(lid));
+    return valid ? (lid >> 4) * c4 + (lid & 15u) * 4u + soff : 0x7fffffffu;
+  }
   // pair G = tiles 2G (v[0..3], rows 32G + 4 g4 + r) and 2G+1 (v[4..7], rows + 16).
   // The lane's offsets are recomputed here (a few VALU in the MFMA shadows)
   // instead of living in VGPRs through the whole tile.
   template <int G>
   __device__ __forceinline__ void pair(const Op& v) {
     if (!on) return;
-    unsigned lid = __lane_id();
-    asm volatile("" : "+v"(lid));
-    const unsigned vo = valid ? (lid >> 4) * 4u * ld4 + (lid & 15u) * 4u + soff : 0x7fffffffu;
+    const unsigned vo = lane_off();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, (int)vo,
-                                            (int)((32 * G + r) * ld4), NERF_ACT_STORE_AUX);
+                                            (int)(2 * G * ts + r * rstr), NERF_ACT_STORE_AUX);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + r]), rs, (int)vo,
-                                            (int)((32 * G + 16 + r) * ld4), NERF_ACT_STORE_AUX);
+                                            (int)((2 * G + 1) * ts + r * rstr),
+                                            NERF_ACT_STORE_AUX);
     }
     if (bits) {   // bit 4t + r of the block word = (h > 0): post-ReLU h >= 0
       unsigned m = 0u;
@@ -393,7 +436,7 @@ struct ActStore {
       } else {
         wb |= m << 8;
         if (valid)
-          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)wb, rb, (int)(lid * 2u),
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)wb, rb, (int)(__lane_id() * 2u),
                                                 (int)(sboff + (G >> 1) * 128), 0);
       }
     }
@@ -407,7 +450,7 @@ struct X3TrainOut {
   unsigned short* bits[9];      // ReLU bits of h0..h7 (x3_layer_kernel MT 16) and views (MT 8)
   float* amax;                  // [12]: raised to max |.| of h0..h7 (0-7), feature (8), xyz
                                 // encoding (9), view encoding (10), views (11)
-  int64_t ld;                   // row stride of every output, floats
+  Lay lay;                      // every output's layout (row stride / T16 block stride)
 };
 
 // Encoding rows of the training forward: the feature index (freq.py's column
@@ -432,9 +475,8 @@ __device__ __forceinline__ int enc_dir_row(int g, int j) {
 // is enforced by the launchers: the sum cannot wrap), and a null output (the
 // skipped feature / DF rows) gets num_records 0: every store through it is
 // dropped even if a path forgets the ActStore::on test.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, int64_t ld) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, p ? (int)((int64_t)rows * ld * 4) : 0,
-                                           0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, const Lay& L) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, p ? L.extent(rows) : 0, 0x00020000);
 }
 
 // LIST: the samples are the flat indices list[0 .. *count) (ray * S + step,
@@ -515,13 +557,12 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the encoding rows (the wgrad operand of layers 0 and 5)
     int i10 = 10;
     asm volatile("" : "+s"(i10));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i10], 64, to.ld);
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i10], 64, to.lay);
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const unsigned vo = valid ? (unsigned)(((int64_t)enc_xyz_row(g4, q, j) * to.ld + gs) * 4)
-                                  : 0x7fffffffu;
+        const unsigned vo = valid ? to.lay.elem(enc_xyz_row(g4, q, j), gs) : 0x7fffffffu;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(encf[q][j]), rs, (int)vo, 0, 0);
       }
   }
@@ -539,13 +580,12 @@ __device__ __forceinline__ void mlp_x3_body(
       // pointers would not fit the SGPR budget)
       int Li = L;
       asm volatile("" : "+s"(Li));
-      st.rs = rows_rsrc(to.act[Li], rows, to.ld);
+      st.rs = rows_rsrc(to.act[Li], rows, to.lay);
       st.on = to.act[Li] != nullptr;   // the feature rows may be skipped (act[8] null)
       st.bits = L < 8;
       st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)to.bits[Li < 8 ? Li : 0], 0,
                                                 L < 8 ? 0x7fffffff : 0, 0x00020000);
-      st.soff = (unsigned)((tile * kX3Tile + wv * 16) * 4);
-      st.ld4 = (unsigned)(to.ld * 4);
+      st.set_lay(to.lay, tile, wv);
       st.sboff = (unsigned)(((tile * 8 + wv) * 4) * 64 * 2);
       st.wb = 0u;
       st.valid = valid;
@@ -653,11 +693,10 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the view-encoding rows (the views layer's wgrad operand)
     int i11 = 11;
     asm volatile("" : "+s"(i11));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i11], 32, to.ld);
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i11], 32, to.lay);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const unsigned vo = valid ? (unsigned)(((int64_t)enc_dir_row(g4, j) * to.ld + gs) * 4)
-                                : 0x7fffffffu;
+      const unsigned vo = valid ? to.lay.elem(enc_dir_row(g4, j), gs) : 0x7fffffffu;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dirf[j]), rs, (int)vo, 0, 0);
     }
     amax_to_lds(10, op_absmax(dirf));
@@ -698,9 +737,11 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the views output rows, its ReLU bits (MT 8) and max
     int i9 = 9;
     asm volatile("" : "+s"(i9));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i9], 128, to.ld);
-    const unsigned ld4 = (unsigned)(to.ld * 4);
-    const unsigned voff = valid ? (unsigned)(((int64_t)4 * g4 * to.ld + gs) * 4) : 0x7fffffffu;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i9], 128, to.lay);
+    ActStore sv;
+    sv.valid = valid;
+    sv.set_lay(to.lay, tile, wave);
+    const unsigned voff = sv.lane_off();
     float vmax = 0.0f;
 #pragma unroll
     for (int u0 = 0; u0 < 8; u0 += 4) {
@@ -711,7 +752,7 @@ __device__ __forceinline__ void mlp_x3_body(
         for (int r = 0; r < 4; ++r) {
           const float v = acc8[u0 + t][r];
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff,
-                                                (int)((16 * (u0 + t) + r) * ld4), 0);
+                                                (int)((u0 + t) * sv.ts + r * sv.rstr), 0);
           wb |= min(__float_as_uint(v), 1u) << (4 * t + r);
           vmax = fmaxf(vmax, v);
         }
@@ -824,8 +865,8 @@ struct X3BwdIO {
   const unsigned short* bits[9];  // ReLU bits of h0..h7 (m_tiles 16), of the views output (8)
   float* d[12];                   // 0..7: D0..D7, 8: DF, 9: d_hv, 10: d_enc (layer 5), 11: (layer 0)
   float* dmax;                    // raised: [i] = max |D_i|, [8] max |DF|, [10] max |d_hv|
-  int64_t ld;
-  float* d_raw_t;                 // nullable: rows 0..3 (stride ld) = d sigma, d rgb (x, y, z)
+  float* d_raw_t;                 // nullable: rows 0..3 = d sigma, d rgb (x, y, z)
+  Lay lay;                        // every output's layout (row stride / T16 block stride)
 };
 
 // Epilogue of a dgrad layer, fused into its last slice: 2^-shift * acc (exact),
@@ -995,23 +1036,22 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   // (unwritten) mask words of their tile say, and no max |.| sees them
   float4 dr = io.d_raw[gl];
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (io.d_raw_t && g4 == 0 && valid) {   // d raw feature-major: the heads' wgrad operands
-    float* t = io.d_raw_t + gs;
-    t[0] = dr.w;
-    t[io.ld] = dr.x;
-    t[2 * io.ld] = dr.y;
-    t[3 * io.ld] = dr.z;
+  if (io.d_raw_t && g4 == 0 && valid) {   // d raw as 4 rows: the heads' wgrad operands
+    char* t = reinterpret_cast<char*>(io.d_raw_t);
+    *reinterpret_cast<float*>(t + io.lay.elem(0, gs)) = dr.w;
+    *reinterpret_cast<float*>(t + io.lay.elem(1, gs)) = dr.x;
+    *reinterpret_cast<float*>(t + io.lay.elem(2, gs)) = dr.y;
+    *reinterpret_cast<float*>(t + io.lay.elem(3, gs)) = dr.z;
   }
   // outputs / masks of this (tile, wave): pointers loaded at their layer
   auto store_for = [&](int k, int rows) {
     ActStore st;
     int ki = k;
     asm volatile("" : "+s"(ki));
-    st.rs = rows_rsrc(io.d[ki], rows, io.ld);
+    st.rs = rows_rsrc(io.d[ki], rows, io.lay);
     st.on = io.d[ki] != nullptr;       // DF may be skipped (d[8] null)
     st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
-    st.soff = (unsigned)((tile * kX3Tile + wave * 16) * 4);
-    st.ld4 = (unsigned)(io.ld * 4);
+    st.set_lay(io.lay, tile, wave);
     st.sboff = 0u;
     st.wb = 0u;
     st.bits = false;
@@ -1700,11 +1740,16 @@ __device__ __forceinline__ void wgrad_dma_body(
 
   // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1).
   // Element (r, p) of an operand: r * ld + (p >> 4) * bs + (p & 15) (bs 16:
-  // feature-major rows; 16 * rows with ld 16: the 16-sample block layout). A K
-  // step's block offset rides in soffset, the lane's row and column in voffset;
-  // num_records = the operand's extent (rows past M / N read 0)
-  const int nbA = (int)((((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16) * 4);
-  const int nbB = (int)((((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16) * 4);
+  // feature-major rows), or Lay::rowpart(r) + (p >> 4) * bs + (p & 15) (the T16
+  // layout, bs = its block stride). A K step's block offset rides in soffset,
+  // the lane's row and column in voffset; num_records = the operand's extent
+  // (rows past M / N read 0)
+  // bs != 16: the T16 layout (Lay), rows permuted inside their 16-row groups
+  const bool ta = bsa != 16, tb = bsb != 16;
+  const int nbA = ta ? (int)(((P / 16 - 1) * bsa + ((M + 15) & ~15) * 16) * 4)
+                     : (int)((((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16) * 4);
+  const int nbB = tb ? (int)(((P / 16 - 1) * bsb + ((N + 15) & ~15) * 16) * 4)
+                     : (int)((((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16) * 4);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nbA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
   unsigned voA[4], voB[4];
@@ -1713,10 +1758,10 @@ __device__ __forceinline__ void wgrad_dma_body(
     const int q = 4 * wave + i, t = q >> 1, h = q & 1;
     const int col = 8 * (lane >> 4) + 4 * h;     // sample of the K step, 0 .. 31
     const int ra = m0 + 16 * t + (lane & 15), rb = n0 + 16 * t + (lane & 15);
-    voA[i] = ra < M ? (unsigned)(((int64_t)ra * lda + (col >> 4) * bsa + (col & 15)) * 4)
-                    : (unsigned)nbA;
-    voB[i] = rb < N ? (unsigned)(((int64_t)rb * ldb + (col >> 4) * bsb + (col & 15)) * 4)
-                    : (unsigned)nbB;
+    const int64_t rowa = ta ? Lay::rowpart(ra) : (int64_t)ra * lda;
+    const int64_t rowb = tb ? Lay::rowpart(rb) : (int64_t)rb * ldb;
+    voA[i] = ra < M ? (unsigned)((rowa + (col >> 4) * bsa + (col & 15)) * 4) : (unsigned)nbA;
+    voB[i] = rb < N ? (unsigned)((rowb + (col >> 4) * bsb + (col & 15)) * 4) : (unsigned)nbB;
   }
   // piece I of granule g: A (g even) or B (g odd) of step g >> 1, into slot g % 5
   auto issue_piece = [&](int g, auto Ic) {
@@ -2101,6 +2146,22 @@ extern "C" int nerf_mlp_train_forward_x3(const float* w_slices, const float* w_h
                                         stream);
 }
 
+// the training kernels' output layout (Lay): feature-major rows need ld >= P and
+// 256 rows within 2 GiB; T16 (bs > 0) needs whole 16-row groups per block
+// (bs % 256 == 0) and the buffer within 2 GiB. 32-bit offsets either way.
+static bool lay_ok(int64_t ld, int64_t bs, int64_t P) {
+  if (bs == 0) return ld >= P && (int64_t)256 * ld * 4 < (1ll << 31);
+  const int64_t nblk = cdiv(P, kX3Tile) * 8;
+  return bs > 0 && bs % 256 == 0 && nblk * bs * 4 < (1ll << 31);
+}
+static Lay make_lay(int64_t ld, int64_t bs, int64_t P) {
+  Lay L;
+  L.ld = bs ? 16 : ld;
+  L.bs = bs;
+  L.nblk = cdiv(P, kX3Tile) * 8;
+  return L;
+}
+
 extern "C" int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float* w_head,
                                               const float* rays_o, const float* rays_d,
                                               const float* z, int64_t z_stride, int64_t n, int S,
@@ -2110,13 +2171,12 @@ extern "C" int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float
                "nerf_mlp_train_forward_x3: null pointer");
   NERF_REQUIRE(n >= 0 && S >= 1 && z_stride >= 0, "nerf_mlp_train_forward_x3: bad size");
   const int64_t P = n * S;
-  NERF_REQUIRE(out->ld >= P, "nerf_mlp_train_forward_x3: bad size");
+  NERF_REQUIRE(lay_ok(out->ld, out->bs, P), "nerf_mlp_train_forward_x3: bad layout");
   for (int i = 0; i < 12; ++i)   // act[8] (the feature rows) may be null: not stored
     NERF_REQUIRE(i == 8 || out->act[i] != nullptr, "nerf_mlp_train_forward_x3: null output rows");
   for (int i = 0; i < 9; ++i)
     NERF_REQUIRE(out->bits[i] != nullptr, "nerf_mlp_train_forward_x3: null relu bits");
-  NERF_REQUIRE((int64_t)256 * out->ld * 4 < (1ll << 31),
-               "nerf_mlp_train_forward_x3: rows too long for 32-bit offsets");
+
   NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
                    ((uintptr_t)raw & 15) == 0,
                "nerf_mlp_train_forward_x3: weights/raw must be 16-byte aligned");
@@ -2129,7 +2189,7 @@ extern "C" int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float
   for (int i = 0; i < 12; ++i) to.act[i] = out->act[i];
   for (int i = 0; i < 9; ++i) to.bits[i] = out->bits[i];
   to.amax = out->amax;
-  to.ld = out->ld;
+  to.lay = make_lay(out->ld, out->bs, P);
   hipLaunchKernelGGL(mlp_x3_train_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
                      as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
                      z_stride, P, S, (float4*)raw, to);
@@ -2141,15 +2201,14 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
                                           nerf_stream_t stream) {
   NERF_REQUIRE(w_slices && w_head && io && io->d_raw && io->dmax,
                "nerf_mlp_train_backward_x3: null pointer");
-  NERF_REQUIRE(P >= 0 && io->ld >= P, "nerf_mlp_train_backward_x3: bad size");
+  NERF_REQUIRE(P >= 0 && lay_ok(io->ld, io->bs, P), "nerf_mlp_train_backward_x3: bad layout");
   for (int i = 0; i < 10; ++i)   // d[8] (DF) may be null: not stored
     NERF_REQUIRE(i == 8 || io->d[i] != nullptr, "nerf_mlp_train_backward_x3: null output rows");
   if (with_enc)
     NERF_REQUIRE(io->d[10] && io->d[11], "nerf_mlp_train_backward_x3: null encoding rows");
   for (int i = 0; i < 9; ++i)
     NERF_REQUIRE(io->bits[i] != nullptr, "nerf_mlp_train_backward_x3: null relu bits");
-  NERF_REQUIRE((int64_t)256 * io->ld * 4 < (1ll << 31),
-               "nerf_mlp_train_backward_x3: rows too long for 32-bit offsets");
+
   NERF_REQUIRE(((uintptr_t)w_slices & 15) == 0 && ((uintptr_t)w_head & 15) == 0 &&
                    ((uintptr_t)io->d_raw & 15) == 0,
                "nerf_mlp_train_backward_x3: weights/d_raw must be 16-byte aligned");
@@ -2163,7 +2222,7 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
   for (int i = 0; i < 9; ++i) b.bits[i] = io->bits[i];
   for (int i = 0; i < 12; ++i) b.d[i] = io->d[i];
   b.dmax = io->dmax;
-  b.ld = io->ld;
+  b.lay = make_lay(io->ld, io->bs, P);
   b.d_raw_t = io->d_raw_t;
   if (with_enc)
     hipLaunchKernelGGL(mlp_x3_bwd_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
@@ -2280,8 +2339,10 @@ extern "C" int nerf_x3_layer_ex(const float* w_packed, const int* w_scale, int m
 
 static bool wgrad_dma_ok(const float* A, int64_t lda, int M, const float* B, int64_t ldb, int N,
                          int64_t P, int64_t bsa = 16, int64_t bsb = 16) {
-  const int64_t ea = ((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16;   // operand extents
-  const int64_t eb = ((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16;
+  const int64_t ea = bsa != 16 ? (P / 16 - 1) * bsa + ((M + 15) & ~15) * 16   // operand extents
+                               : ((int64_t)M - 1) * lda + (P / 16 - 1) * bsa + 16;
+  const int64_t eb = bsb != 16 ? (P / 16 - 1) * bsb + ((N + 15) & ~15) * 16
+                               : ((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16;
   return P % 32 == 0 && lda % 4 == 0 && ldb % 4 == 0 && bsa % 4 == 0 && bsb % 4 == 0 &&
          ((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 &&
          ea * 4 < ((int64_t)1 << 31) && eb * 4 < ((int64_t)1 << 31);
@@ -2323,8 +2384,8 @@ extern "C" int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const in
     // feature-major rows hold every sample (ld >= P); in the block layout a
     // block holds every row (bs >= 16 rows, ld = 16)
     NERF_REQUIRE(d.A && d.B && d.amax_a && d.amax_b && d.part && d.M > 0 && d.N > 0 &&
-                     d.P >= 0 && (bsa == 16 ? d.lda >= d.P : d.lda == 16 && bsa >= 16 * d.M) &&
-                     (bsb == 16 ? d.ldb >= d.P : d.ldb == 16 && bsb >= 16 * d.N) && ldo >= d.N &&
+                     d.P >= 0 && (bsa == 16 ? d.lda >= d.P : bsa % 256 == 0 && bsa >= 16 * d.M) &&
+                     (bsb == 16 ? d.ldb >= d.P : bsb % 256 == 0 && bsb >= 16 * d.N) && ldo >= d.N &&
                      d.ldpart >= (int64_t)(d.M - 1) * ldo + d.N &&
                      (!d.bias_part || d.ldbias >= d.M),
                  "nerf_x3_wgrad_batch: bad descriptor");

@@ -874,21 +874,31 @@ __global__ __launch_bounds__(64 * kEncMaxWaves) void freq_encode_fm_kernel(
   }
 }
 
+// Element (row, p) of an [rows][P] operand, floats: feature-major rows
+// (bs == 0: row * ld + p) or the training kernels' T16 layout (bs > 0: block
+// stride bs, rows permuted inside their 16-row groups; mlp_x3.hip Lay).
+__device__ __forceinline__ int64_t lay_idx(int row, int64_t p, int64_t ld, int64_t bs) {
+  return bs ? (p >> 4) * bs + ((row >> 4) * 256 + (row & 3) * 64 + ((row >> 2) & 3) * 16) + (p & 15)
+            : (int64_t)row * ld + p;
+}
+
 // d x_c = d_enc[c] + sum_f 2^f (cos(2^f x_c) d_sin - sin(2^f x_c) d_cos): the
 // chain rule through the encoding (autograd of freq.py's cat of sin/cos).
 // With d_enc2, d_enc = d_enc + d_enc2 elementwise first (the encoding feeds two
 // layers: autograd's sum of their input gradients). With enc (the forward's
-// encoding rows, stride ldd), sin / cos are read from it instead of recomputed
-// (the same sincosf values: it is what the forward wrote).
+// encoding rows, layout (lde, bse)), sin / cos are read from it instead of
+// recomputed (the same sincosf values: it is what the forward wrote). d_enc /
+// d_enc2 in layout (ldd, bsd); lay_idx.
 __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
-    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
-    const float* __restrict__ enc, const float* __restrict__ x, int64_t ldx, int64_t P, int L,
-    float* __restrict__ dx) {
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd, int64_t bsd,
+    const float* __restrict__ enc, int64_t lde, int64_t bse, const float* __restrict__ x,
+    int64_t ldx, int64_t P, int L, float* __restrict__ dx) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   auto de = [&](int row) {
-    float v = d_enc[row * ldd + p];
-    if (d_enc2) v = v + d_enc2[row * ldd + p];
+    const int64_t i = lay_idx(row, p, ldd, bsd);
+    float v = d_enc[i];
+    if (d_enc2) v = v + d_enc2[i];
     return v;
   };
 #pragma unroll
@@ -899,8 +909,8 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
       const float k = (float)(1 << f);
       float sn, cs;
       if (enc) {
-        sn = enc[(3 + 6 * f + c) * ldd + p];
-        cs = enc[(6 + 6 * f + c) * ldd + p];
+        sn = enc[lay_idx(3 + 6 * f + c, p, lde, bse)];
+        cs = enc[lay_idx(6 + 6 * f + c, p, lde, bse)];
       } else {
         sincosf(v * k, &sn, &cs);
       }
@@ -918,15 +928,16 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_kernel(
 // together; the runtime loop exposes one load latency per band)
 template <int LC>
 __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
-    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
-    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P, int Lr,
-    float* __restrict__ dz) {
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd, int64_t bsd,
+    const float* __restrict__ enc, int64_t lde, int64_t bse, const float* __restrict__ rays_d,
+    int S, int64_t P, int Lr, float* __restrict__ dz) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   const int L = LC > 0 ? LC : Lr;
   auto de = [&](int row) {
-    float v = d_enc[row * ldd + p];
-    if (d_enc2) v = v + d_enc2[row * ldd + p];
+    const int64_t i = lay_idx(row, p, ldd, bsd);
+    float v = d_enc[i];
+    if (d_enc2) v = v + d_enc2[i];
     return v;
   };
   const int64_t ray = p / S;
@@ -937,8 +948,8 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
 #pragma unroll
     for (int f = 0; f < L; ++f) {
       const float k = (float)(1 << f);
-      const float sn = enc[(3 + 6 * f + c) * ldd + p];
-      const float cs = enc[(6 + 6 * f + c) * ldd + p];
+      const float sn = enc[lay_idx(3 + 6 * f + c, p, lde, bse)];
+      const float cs = enc[lay_idx(6 + 6 * f + c, p, lde, bse)];
       const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
       g = g + ds * k;
     }
@@ -953,9 +964,9 @@ __global__ __launch_bounds__(256) void freq_encode_fm_backward_dz_kernel(
 // flight), and lane s of wave 0 adds the three products in c order through LDS
 // (the same operations in the same order as the one-thread-per-sample kernel).
 __global__ __launch_bounds__(192) void freq_encode_fm_backward_dz3_kernel(
-    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd,
-    const float* __restrict__ enc, const float* __restrict__ rays_d, int S, int64_t P,
-    float* __restrict__ dz) {
+    const float* __restrict__ d_enc, const float* __restrict__ d_enc2, int64_t ldd, int64_t bsd,
+    const float* __restrict__ enc, int64_t lde, int64_t bse, const float* __restrict__ rays_d,
+    int S, int64_t P, float* __restrict__ dz) {
   constexpr int L = 10;
   __shared__ float t3[3][64];
   const int c = threadIdx.x >> 6, s = threadIdx.x & 63;
@@ -963,16 +974,17 @@ __global__ __launch_bounds__(192) void freq_encode_fm_backward_dz3_kernel(
   const bool ok = p < P;
   const int64_t pp = ok ? p : 0;
   auto de = [&](int row) {
-    float v = d_enc[row * ldd + pp];
-    if (d_enc2) v = v + d_enc2[row * ldd + pp];
+    const int64_t i = lay_idx(row, pp, ldd, bsd);
+    float v = d_enc[i];
+    if (d_enc2) v = v + d_enc2[i];
     return v;
   };
   float g = de(c);
 #pragma unroll
   for (int f = 0; f < L; ++f) {
     const float k = (float)(1 << f);
-    const float sn = enc[(3 + 6 * f + c) * ldd + pp];
-    const float cs = enc[(6 + 6 * f + c) * ldd + pp];
+    const float sn = enc[lay_idx(3 + 6 * f + c, pp, lde, bse)];
+    const float cs = enc[lay_idx(6 + 6 * f + c, pp, lde, bse)];
     const float ds = de(3 + 6 * f + c) * cs - de(6 + 6 * f + c) * sn;
     g = g + ds * k;
   }
@@ -1206,36 +1218,47 @@ int nerf_freq_encode_fm(const float* x, int64_t ldx, int64_t P, int n_freq, floa
 
 int nerf_freq_encode_fm_backward(const float* d_enc, int64_t ldd, const float* x, int64_t ldx,
                                  int64_t P, int n_freq, float* dx, nerf_stream_t stream) {
-  return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, nullptr, x, ldx, P, n_freq, dx,
-                                          stream);
+  return nerf_freq_encode_fm_backward_sum(d_enc, nullptr, ldd, 0, nullptr, ldd, 0, x, ldx, P,
+                                          n_freq, dx, stream);
+}
+
+// an operand layout (ld, bs) as lay_idx reads it: feature-major rows need ld >= P
+static bool enc_lay_ok(int64_t ld, int64_t bs, int64_t P) {
+  return bs == 0 ? ld >= P : bs > 0 && bs % 256 == 0;
 }
 
 int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                    const float* enc, const float* rays_d, int S, int64_t P,
-                                    int n_freq, float* dz, nerf_stream_t stream) {
+                                    int64_t bsd, const float* enc, int64_t lde, int64_t bse,
+                                    const float* rays_d, int S, int64_t P, int n_freq, float* dz,
+                                    nerf_stream_t stream) {
   NERF_REQUIRE(d_enc && enc && rays_d && dz, "nerf_freq_encode_fm_backward_dz: null pointer");
-  NERF_REQUIRE(P >= 0 && S >= 1 && P % S == 0 && ldd >= P && n_freq >= 0 && n_freq <= 24,
+  NERF_REQUIRE(P >= 0 && S >= 1 && P % S == 0 && enc_lay_ok(ldd, bsd, P) &&
+                   enc_lay_ok(lde, bse, P) && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm_backward_dz: bad size");
   if (P == 0) return 0;
   if (n_freq == 10)   // the xyz encoding (L = 10)
     hipLaunchKernelGGL(freq_encode_fm_backward_dz3_kernel, dim3((unsigned)cdiv(P, 64)),
-                       dim3(192), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P, dz);
+                       dim3(192), 0, as_stream(stream), d_enc, d_enc2, ldd, bsd, enc, lde, bse,
+                       rays_d, S, P, dz);
   else
     hipLaunchKernelGGL(freq_encode_fm_backward_dz_kernel<0>, dim3((unsigned)cdiv(P, 256)),
-                       dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, enc, rays_d, S, P,
-                       n_freq, dz);
+                       dim3(256), 0, as_stream(stream), d_enc, d_enc2, ldd, bsd, enc, lde, bse,
+                       rays_d, S, P, n_freq, dz);
   return check_launch("freq_encode_fm_backward_dz_kernel");
 }
 
 int nerf_freq_encode_fm_backward_sum(const float* d_enc, const float* d_enc2, int64_t ldd,
-                                     const float* enc, const float* x, int64_t ldx, int64_t P,
-                                     int n_freq, float* dx, nerf_stream_t stream) {
+                                     int64_t bsd, const float* enc, int64_t lde, int64_t bse,
+                                     const float* x, int64_t ldx, int64_t P, int n_freq,
+                                     float* dx, nerf_stream_t stream) {
   NERF_REQUIRE(d_enc && x && dx, "nerf_freq_encode_fm_backward: null pointer");
-  NERF_REQUIRE(P >= 0 && ldx >= 3 && ldd >= P && n_freq >= 0 && n_freq <= 24,
+  NERF_REQUIRE(P >= 0 && ldx >= 3 && enc_lay_ok(ldd, bsd, P) &&
+                   (!enc || enc_lay_ok(lde, bse, P)) && n_freq >= 0 && n_freq <= 24,
                "nerf_freq_encode_fm_backward: bad size");
   if (P == 0) return 0;
   hipLaunchKernelGGL(freq_encode_fm_backward_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0,
-                     as_stream(stream), d_enc, d_enc2, ldd, enc, x, ldx, P, n_freq, dx);
+                     as_stream(stream), d_enc, d_enc2, ldd, bsd, enc, lde, bse, x, ldx, P, n_freq,
+                     dx);
   return check_launch("freq_encode_fm_backward_kernel");
 }
 

@@ -428,13 +428,13 @@ class _BwdIO(ctypes.Structure):
     """NerfX3BwdIO (include/nerfhip.h)."""
     _fields_ = [("d_raw", ctypes.c_void_p), ("bits", ctypes.c_void_p * 9),
                 ("d", ctypes.c_void_p * 12), ("dmax", ctypes.c_void_p), ("ld", ctypes.c_int64),
-                ("d_raw_t", ctypes.c_void_p)]
+                ("d_raw_t", ctypes.c_void_p), ("bs", ctypes.c_int64)]
 
 
 class _TrainOut(ctypes.Structure):
     """NerfX3TrainOut (include/nerfhip.h)."""
     _fields_ = [("act", ctypes.c_void_p * 12), ("bits", ctypes.c_void_p * 9),
-                ("amax", ctypes.c_void_p), ("ld", ctypes.c_int64)]
+                ("amax", ctypes.c_void_p), ("ld", ctypes.c_int64), ("bs", ctypes.c_int64)]
 
 
 _PACKERS = {}
@@ -547,20 +547,25 @@ def _dma_ok(t):
     return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
 
 
-BLOCK = 16   # samples per block of the block layout
+BLOCK = 16   # samples per block of the T16 layout
 
 
 class BlockRows:
-    """Rows r0 .. r0 + M of a [R, P] activation stored in the 16-sample block
-    layout: buf is [nb, R, 16] (nb = ceil(P / 128) * 8 blocks: whole 128-sample
-    tiles), element (r, p) at buf[p // 16, r0 + r, p % 16]. A wave of the fused
-    training kernels owns 16 samples, so every row it writes is one contiguous
-    64-B run and a (wave, layer) output one contiguous 16 KiB region; a K step
-    of the weight gradients (32 samples) reads two contiguous regions per
-    operand instead of one 128-B run per row (NerfWgradDesc bsa / bsb)."""
+    """Rows r0 .. r0 + M of an [R, P] activation in the T16 layout of the fused
+    training kernels (mlp_x3.hip Lay; NerfX3TrainOut.bs): buf is [nb, R, 16]
+    (nb = ceil(P / 128) * 8 blocks of 16 samples: whole 128-sample tiles, R a
+    multiple of 16); inside a block each 16-row group is one 1-KiB tile in
+    which row 16 t + 4 g + q of sample s sits at t * 256 + q * 64 + g * 16 + s.
+    So element q of every lane of a 16 x 16 MFMA accumulator tile (lane
+    16 g + s holds rows 4 g .. 4 g + 3 of sample s) is 256 contiguous bytes: the
+    training kernels write their outputs as whole lines, one store instruction
+    per accumulator element, and a K step of the weight gradients (32 samples)
+    reads two contiguous runs per operand (NerfWgradDesc bsa / bsb). Operands
+    start on 16-row groups (r0 % 16 == 0)."""
 
     def __init__(self, buf, r0, M, P):
         assert buf.dim() == 3 and buf.shape[2] == BLOCK and buf.is_contiguous()
+        assert buf.shape[1] % 16 == 0 and r0 % 16 == 0
         assert 0 <= r0 and r0 + M <= buf.shape[1] and buf.shape[0] * BLOCK >= P
         self.buf, self.r0, self.M, self.P = buf, int(r0), int(M), int(P)
         self.shape = (self.M, self.P)
@@ -568,11 +573,12 @@ class BlockRows:
 
     @staticmethod
     def alloc(R, P, dev):
+        R = -(-R // 16) * 16
         nb = -(-P // 128) * (128 // BLOCK)
         return BlockRows(torch.empty((nb, R, BLOCK), device=dev, dtype=torch.float32), 0, R, P)
 
     def rows(self, a, b):
-        """Rows a .. b of this operand (a view)."""
+        """Rows a .. b of this operand (a view; a on a 16-row group)."""
         return BlockRows(self.buf, self.r0 + a, b - a, self.P)
 
     def data_ptr(self):
@@ -581,28 +587,38 @@ class BlockRows:
     def numel(self):   # the whole buffer: the operand's extent lies inside it
         return self.buf.numel()
 
-    def stride(self, dim):   # NerfWgradDesc lda (the row stride) and bs
+    def stride(self, dim):   # NerfWgradDesc lda (unused in T16) and bs
         return BLOCK if dim == 0 else 1
 
     @property
     def block_stride(self):
         return BLOCK * self.buf.shape[1]
 
+    def _grid(self):
+        nb, R, _ = self.buf.shape
+        return self.buf.view(nb, R // 16, 4, 4, BLOCK)   # [b, t, q, g, s]
+
     def dense(self):
         """The same rows feature-major, [M, P] (tests, the fallback paths)."""
-        b = self.buf[:, self.r0:self.r0 + self.M, :]
-        return b.permute(1, 0, 2).reshape(self.M, -1)[:, :self.P]
+        nb, R, _ = self.buf.shape
+        full = self._grid().permute(1, 3, 2, 0, 4).reshape(R, nb * BLOCK)   # row 16t + 4g + q
+        return full[self.r0:self.r0 + self.M, :self.P]
 
     @staticmethod
     def from_dense(A, R=None):
-        """A [M, P] copied into a new block-layout buffer (tests, tools)."""
+        """A [M, P] copied into a new T16 buffer (tests, tools)."""
         M, P = A.shape
         out = BlockRows.alloc(R or M, P, A.device)
-        nb = out.buf.shape[0]
-        full = torch.zeros((M, nb * BLOCK), device=A.device, dtype=torch.float32)
-        full[:, :P] = A
-        out.buf[:, :M, :] = full.view(M, nb, BLOCK).permute(1, 0, 2)
+        nb, Rr, _ = out.buf.shape
+        full = torch.zeros((Rr, nb * BLOCK), device=A.device, dtype=torch.float32)
+        full[:M, :P] = A
+        out._grid().copy_(full.view(Rr // 16, 4, 4, nb, BLOCK).permute(3, 0, 2, 1, 4))
         return out.rows(0, M)
+
+
+def rows_of(t, a, b):
+    """Rows a .. b of a feature-major tensor or a BlockRows operand."""
+    return t.rows(a, b) if isinstance(t, BlockRows) else t[a:b]
 
 
 WGRAD_COST_FLOOR = int(_os.environ.get("NERF_WGRAD_COST_FLOOR", "512"))
@@ -786,6 +802,40 @@ def _padded(W, cols, K):
     return out
 
 
+# The fused forward + fused backward write their rows in the T16 layout
+# (BlockRows: whole-line stores, contiguous weight-gradient K steps);
+# NERF_TRAIN_T16=0 keeps them feature-major. The layer launches are
+# feature-major only, so T16 needs both fused kernels.
+T16 = _os.environ.get("NERF_TRAIN_T16", "1") != "0"
+# the forward's rows in one T16 buffer (16-row groups): E = [enc 64 | h4 256],
+# V = [h7 256 | view enc 32], HV 128, then h0..h3, h5, h6
+_FWD_ROWS = {"E": (0, 320), "V": (320, 608), "HV": (608, 736)}
+_FWD_H = {0: 736, 1: 992, 2: 1248, 3: 1504, 5: 1760, 6: 2016}
+_FWD_R = 2272
+# the fused backward's rows: [d_hv 128 | d raw 4] (hx), D0..D7, d_enc5, d_enc0
+_BWD_HX, _BWD_D, _BWD_E5, _BWD_E0, _BWD_R = 0, 144, 2192, 2256, 2320
+
+
+def _t16_ok(P):
+    """T16 for a pass of P samples: the larger (backward) buffer within the 2 GiB
+    of the kernels' 32-bit buffer offsets (P <= 229 376: a 1024-ray C3 step's
+    fine pass is 196 608; larger passes stay feature-major)."""
+    return T16 and 0 < P and -(-P // 128) * 128 * _BWD_R * 4 < (1 << 31)
+
+
+def _fwd_rows_t16(buf, P):
+    """E, H (h4 / h7 as rows of E / V), V, HV as BlockRows over one T16 buffer."""
+    fb = BlockRows(buf, 0, _FWD_R, P)
+    E = fb.rows(*_FWD_ROWS["E"])
+    V = fb.rows(*_FWD_ROWS["V"])
+    HV = fb.rows(*_FWD_ROWS["HV"])
+    H = [fb.rows(r, r + 256) if i in _FWD_H else None for i, r in
+         ((i, _FWD_H.get(i, 0)) for i in range(8))]
+    H[4] = E.rows(64, 320)
+    H[7] = V.rows(0, 256)
+    return E, H, V, HV
+
+
 class NerfMLPFn(torch.autograd.Function):
     """raw [P, 4] = NeRF(cat(freq_encode(pts), freq_encode(dirs))) on x3 kernels.
     Inputs: pts [P, 3] (gradient returned when it requires one), dirs [P, 3]
@@ -806,6 +856,11 @@ class NerfMLPFn(torch.autograd.Function):
         amax, ctx.dmax_buf = stats[:12], stats[12:]
         pts_c = pts.detach().contiguous()
         fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
+        if fused_f and fused_b and _t16_ok(P):
+            ctx.fused_backward = True
+            ctx.streams = _streams_for(params, dev)
+            return NerfMLPFn._forward_fused(ctx, pts, pts_c, dirs, params, None, None, amax,
+                                            None)
         if not fused_f:   # (the fused forward writes the encoding rows itself)
             _encode(pts_c, XYZ_FREQS, E, amax[9:10])               # E[:63] = enc^T
             E[63].zero_()
@@ -857,12 +912,17 @@ class NerfMLPFn(torch.autograd.Function):
         output rows, ReLU bits and max |.|): what the ten layer launches of the
         unfused forward produce, and the backward reads. rays = (rays_o, rays_d,
         z) (RayMLPFn): the samples o + d z of the rays instead of pts / dirs."""
-        dev = E.device
-        P = E.shape[1]
+        dev = amax.device
+        P = (pts_c.shape[0] if rays is None else rays[2].numel())
         stream, head = ctx.streams[:2]
-        V = _act(288, P, dev)      # cat(feature, views enc, 5 zero rows): all from the kernel
+        t16 = E is None    # the T16 layout: every row in one buffer (_fwd_rows_t16)
+        if t16:
+            fbuf = BlockRows.alloc(_FWD_R, P, dev).buf
+            E, H, V, HV = _fwd_rows_t16(fbuf, P)
+        else:
+            V = _act(288, P, dev)   # cat(feature, views enc, 5 zero rows): all from the kernel
+            HV = _act(128, P, dev)
         dirs_c = dirs.detach().contiguous() if rays is None else None
-        HV = _act(128, P, dev)
         bits = torch.empty((8, relu_bits_words(P, 16)), device=dev, dtype=torch.int16)
         bits_v = torch.empty((relu_bits_words(P, 8),), device=dev, dtype=torch.int16)
         raw = torch.empty((P, 4), device=dev, dtype=torch.float32)
@@ -873,7 +933,7 @@ class NerfMLPFn(torch.autograd.Function):
         # views layer's weight gradient is taken through h7 (G = d_hv [h7; enc]^T,
         # then G W_feat^T), which also gives the feature layer's (W_views,feat^T G),
         # so neither the feature rows nor their gradient DF ever reach HBM
-        H[7] = V[0:256]
+        H[7] = rows_of(V, 0, 256)
         out = _TrainOut()
         for i in range(8):
             out.act[i] = H[i].data_ptr()
@@ -881,16 +941,22 @@ class NerfMLPFn(torch.autograd.Function):
         out.act[8] = None
         ctx.v_h7 = True
         out.act[9] = HV.data_ptr()
-        out.act[10] = E[0:64].data_ptr()
-        out.act[11] = V[256:288].data_ptr()
+        out.act[10] = rows_of(E, 0, 64).data_ptr()
+        out.act[11] = rows_of(V, 256, 288).data_ptr()
         out.bits[8] = bits_v.data_ptr()
         out.amax = amax.data_ptr()
-        out.ld = H[0].stride(0)
-        assert all(t.stride(0) == out.ld for t in (E, V, HV)) and H[0].stride(1) == 1
+        if t16:
+            out.ld, out.bs = BLOCK, E.block_stride
+            saved = (fbuf,)
+        else:
+            out.ld, out.bs = H[0].stride(0), 0
+            assert all(t.stride(0) == out.ld for t in (E, V, HV)) and H[0].stride(1) == 1
+            saved = (E, *H[:4], *H[5:], V, HV)
+        ctx.t16 = t16
         if rays is None:
             call("nerf_mlp_train_forward_x3", ptr(stream), ptr(head), ptr(pts_c), ptr(dirs_c),
                  ptr(zero), P, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
-            ctx.save_for_backward(pts_c, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
+            ctx.save_for_backward(pts_c, *saved, amax, bits, bits_v, *params)
             ctx.pts_grad = pts.requires_grad
         else:
             ro, rd, z = rays
@@ -898,18 +964,24 @@ class NerfMLPFn(torch.autograd.Function):
             call("nerf_mlp_train_forward_x3_rays", ptr(stream), ptr(head), ptr(ro), ptr(rd),
                  ptr(z), S, n, S, ctypes.addressof(out), ptr(raw), _lib.stream_of(dev))
             # the rays' directions stand where the points do: d z = sum_c d pts_c d_c
-            ctx.save_for_backward(rd, E, *H[:4], *H[5:], V, HV, amax, bits, bits_v, *params)
+            ctx.save_for_backward(rd, *saved, amax, bits, bits_v, *params)
         ctx.packs = pk
         return raw
 
     @staticmethod
     def backward(ctx, d_raw):
-        pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, bits_v, *params = ctx.saved_tensors
-        H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
-        p = dict(zip(PARAM_NAMES, params))
-        pk = ctx.packs
-        dev = d_raw.device
         P = d_raw.shape[0]
+        t16 = getattr(ctx, "t16", False)
+        if t16:
+            pts, fbuf, amax, bits, bits_v, *params = ctx.saved_tensors
+            E, H, V, HV = _fwd_rows_t16(fbuf, P)
+        else:
+            pts, E, H0, H1, H2, H3, H5, H6, H7, V, HV, amax, bits, bits_v, *params = \
+                ctx.saved_tensors
+            H = [H0, H1, H2, H3, E[64:320], H5, H6, H7]
+        p = dict(zip(PARAM_NAMES, params))
+        pk = getattr(ctx, "packs", None)
+        dev = d_raw.device
         f32 = torch.float32
         grads = {}
         v_h7 = getattr(ctx, "v_h7", False)   # V = [h7; view enc] (fused forward)
@@ -918,9 +990,10 @@ class NerfMLPFn(torch.autograd.Function):
         # fused backward writes d raw feature-major right behind d_hv (rows 128:
         # d sigma, 129..131: d rgb) and no separate alpha tile re-reads h7
         heads_merged = ctx.fused_backward and v_h7
+        bbuf = BlockRows.alloc(_BWD_R, P, dev) if t16 else None   # the backward's rows
         if heads_merged:
-            HX = _act(132, P, dev)
-            d_sig, d_rgb = HX[128:129], HX[129:132]
+            HX = bbuf.rows(_BWD_HX, _BWD_HX + 132) if t16 else _act(132, P, dev)
+            d_sig, d_rgb = rows_of(HX, 128, 129), rows_of(HX, 129, 132)
         else:
             # d_raw^T (the rgb / alpha heads' wgrad operands; the layer launches'
             # d hv K step: 32 rows, 4 of them d_raw)
@@ -949,14 +1022,14 @@ class NerfMLPFn(torch.autograd.Function):
         if ctx.fused_backward:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(
                 d_raw_c, ctx.streams[2:], bits, bits_v, dmax, need_enc, not v_h7,
-                HX if heads_merged else None)
+                HX if heads_merged else None, bbuf)
         else:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
                                                             need_enc)
         post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
         if heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
-            post[wb.add(HX[0:129], V, (dmax[10:11], dmax[12:13]),
+            post[wb.add(rows_of(HX, 0, 129), V, (dmax[10:11], dmax[12:13]),
                         (amax[7:8], amax[10:11]), with_bias=True)] = (
                 "views_G", "views_GA_bias", None)
         elif v_h7:   # G = d_hv [h7; enc]^T: both the views and the feature gradients (below)
@@ -975,7 +1048,8 @@ class NerfMLPFn(torch.autograd.Function):
             # layer 0 reads the 63 encoding rows; the skip layer's [63 encoding
             # rows | h4] are two column blocks of one contiguous [256, 319] result
             # (each with its own scale), so no gradient needs a gather afterwards
-            inp, in_max = (E[0:63], amax[9:10]) if i in (0, 5) else (H[i - 1], amax[i - 1:i])
+            inp, in_max = ((rows_of(E, 0, 63), amax[9:10]) if i in (0, 5)
+                           else (H[i - 1], amax[i - 1:i]))
             s = wb.add(D[i], inp, dmax[i:i + 1], in_max, with_bias=True,
                        width=319 if i == 5 else None)
             post[s] = (f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", None)
@@ -1019,17 +1093,19 @@ class NerfMLPFn(torch.autograd.Function):
             grads["feature_linear.bias"] = Wvf.t() @ sv
         d_pts = None
         if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
-            assert d_enc[0].stride(0) == d_enc[1].stride(0)
-            assert E.stride(0) == d_enc[0].stride(0)
+            def lay(t):   # (row stride, T16 block stride) of an operand
+                return (BLOCK, t.block_stride) if isinstance(t, BlockRows) else (t.stride(0), 0)
+            assert lay(d_enc[0]) == lay(d_enc[1])
+            (ldd, bsd), (lde, bse) = lay(d_enc[0]), lay(E)
             if rays_S:          # pts = the rays' o + d z: straight on to d z
                 d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]),
-                     d_enc[0].stride(0), ptr(E), ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
+                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                     ptr(E), lde, bse, ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
                      _lib.stream_of(dev))
             else:
                 d_pts = torch.empty((P, 3), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]),
-                     d_enc[0].stride(0), ptr(E), ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
+                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                     ptr(E), lde, bse, ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
                      _lib.stream_of(dev))
         if rays_S:
             return (None, None, d_pts, *[grads[n] for n in PARAM_NAMES])
@@ -1078,7 +1154,8 @@ def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
     return d_hv, DF, D, d_enc
 
 
-def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=True, hx=None):
+def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=True, hx=None,
+                         bbuf=None):
     """The same chain as ONE nerf_mlp_train_backward_x3 launch over the
     transposed weight stream (X3BwdStreamPacker): every product's rows written
     feature-major and its max |.| raised, the ReLU masks from the forward's
@@ -1092,11 +1169,19 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=
     d_raw_c = d_raw.detach().to(torch.float32).contiguous()
     if d_raw_c.data_ptr() % 16:
         d_raw_c = d_raw_c.clone()
-    D = [_act(256, P, dev) for _ in range(8)]
-    DF = _act(256, P, dev) if store_df else None
-    d_hv = _act(128, P, dev) if hx is None else hx[0:128]
-    de5 = _act(64, P, dev) if need_enc else None
-    de0 = _act(64, P, dev) if need_enc else None
+    if bbuf is not None:   # T16: every row in the one buffer (_BWD_*), hx its first rows
+        assert hx is not None and not store_df
+        D = [bbuf.rows(_BWD_D + 256 * i, _BWD_D + 256 * (i + 1)) for i in range(8)]
+        DF = None
+        d_hv = hx.rows(0, 128)
+        de5 = bbuf.rows(_BWD_E5, _BWD_E5 + 64) if need_enc else None
+        de0 = bbuf.rows(_BWD_E0, _BWD_E0 + 64) if need_enc else None
+    else:
+        D = [_act(256, P, dev) for _ in range(8)]
+        DF = _act(256, P, dev) if store_df else None
+        d_hv = _act(128, P, dev) if hx is None else hx[0:128]
+        de5 = _act(64, P, dev) if need_enc else None
+        de0 = _act(64, P, dev) if need_enc else None
     io = _BwdIO()
     io.d_raw = d_raw_c.data_ptr()
     for i in range(8):
@@ -1107,13 +1192,17 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=
     io.d[10] = de5.data_ptr() if need_enc else None
     io.d[11] = de0.data_ptr() if need_enc else None
     io.dmax = dmax.data_ptr()
-    io.ld = D[0].stride(0)
-    io.d_raw_t = hx[128].data_ptr() if hx is not None else None
-    assert all(t.stride(0) == io.ld for t in [d_hv] + ([DF] if store_df else []) +
-               ([de5, de0] if need_enc else []))
+    if bbuf is not None:
+        io.ld, io.bs = BLOCK, bbuf.block_stride
+        io.d_raw_t = hx.rows(128, 132).data_ptr()
+    else:
+        io.ld, io.bs = D[0].stride(0), 0
+        io.d_raw_t = hx[128].data_ptr() if hx is not None else None
+        assert all(t.stride(0) == io.ld for t in [d_hv] + ([DF] if store_df else []) +
+                   ([de5, de0] if need_enc else []))
     call("nerf_mlp_train_backward_x3", ptr(stream), ptr(head), P, int(bool(need_enc)),
          ctypes.addressof(io), _lib.stream_of(dev))
-    d_enc = (de5[:63], de0[:63]) if need_enc else None
+    d_enc = (rows_of(de5, 0, 63), rows_of(de0, 0, 63)) if need_enc else None
     return d_hv, DF, D, d_enc
 
 
@@ -1135,12 +1224,15 @@ class RayMLPFn(torch.autograd.Function):
         n, S = z.shape
         P = n * S
         dev = z.device
-        E = _act(320, P, dev)
         stats = torch.zeros(25, device=dev, dtype=torch.float32)   # amax + the backward's dmax
         amax, ctx.dmax_buf = stats[:12], stats[12:]
-        H = [_act(256, P, dev) if i not in (4, 7) else None for i in range(8)]
-        H[4] = E[64:320]                             # h7: V's rows (_forward_fused)
         ctx.fused_backward = FUSED_BACKWARD and P > 0
+        if ctx.fused_backward and _t16_ok(P):   # every row in one T16 buffer (_forward_fused)
+            E = H = None
+        else:
+            E = _act(320, P, dev)
+            H = [_act(256, P, dev) if i not in (4, 7) else None for i in range(8)]
+            H[4] = E[64:320]                             # h7: V's rows (_forward_fused)
         ctx.streams = _streams_for(params, dev)
         ctx.rays_S = S
         pk = None if ctx.fused_backward else _packs_for(params, dev, forward=False, backward=True)

