@@ -3,7 +3,7 @@
 # sub-records) for the tree's library and lib/libnerfhip_<v>.so (VARIANTS),
 # interleaved REPS times.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abh}
 mkdir -p "$OUT"

@@ -5,7 +5,7 @@ schedule changes): the launches alternate A, B, A, B ... on the same inputs
 (lego-like samples: 160 000 rays x 64 depths, synthetic weights), HIP events on
 the launch stream; outputs compared bitwise.
 
-    python tools/ab_x3.py <libA.so> <libB.so> [--reps 20]
+    python tools/ab/ab_x3.py <libA.so> <libB.so> [--reps 20]
 """
 import argparse
 import ctypes as C
@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 
 

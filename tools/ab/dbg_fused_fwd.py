@@ -7,7 +7,7 @@ import sys
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

@@ -3,7 +3,7 @@
 # against the tree's library on the C3 step: bench.py --config c3 (graph),
 # interleaved REPS times, then one rocprofv3 kernel-stats pass per library.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abc3}
 mkdir -p "$OUT"

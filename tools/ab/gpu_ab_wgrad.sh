@@ -3,7 +3,7 @@
 # against the tree's library: the kernel alone at the C3 fine size
 # (tools/train_kernels_bench.py) and the whole C3 step, interleaved twice.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-abw}
 mkdir -p "$OUT"

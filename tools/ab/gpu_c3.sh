@@ -1,7 +1,7 @@
 #!/bin/bash
 # C3 loop: training-MLP GPU tests, the C3 bench line, a kernel-stats profile of it
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-c3}
 mkdir -p $O

@@ -4,7 +4,7 @@
 # launches), then the C3 step of the tree's library against
 # lib/libnerfhip_prev.so, interleaved.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-c3gap}
 mkdir -p "$OUT"

@@ -2,7 +2,7 @@
 # C3 kernel breakdown (rocprof kernel stats of the eager training step) and the
 # kilonerf op tests
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r3c3}
 mkdir -p "$OUT"

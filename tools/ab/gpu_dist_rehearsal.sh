@@ -5,7 +5,7 @@
 # Checks the multi-rank code path end to end (collectives, barriers, max over
 # ranks, rank-0 JSON); RCCL itself needs one GPU per rank (the driver's runs).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp NERF_DIST_BACKEND=gloo
 OUT=gpurun_out/${TAG:-dist2}
 mkdir -p "$OUT"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # quick loop: selected GPU test files ($TESTS), then a short bench ($BENCH_ARGS)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-quick}
 mkdir -p $O

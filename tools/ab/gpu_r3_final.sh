@@ -5,7 +5,7 @@
 # kernels' real HBM traffic). Each GPU step has its own time limit; a failure
 # stops the script.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r3final} bash tools/gpu_check.sh || exit $?
 OUT=gpurun_out/${TAG:-r3final}

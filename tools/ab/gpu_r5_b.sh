@@ -2,7 +2,7 @@
 # round 5: buffer range-check probe, the lego.yaml eval frame (candidate dump),
 # the C3-shape gradient test
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r5_b}
 mkdir -p $O

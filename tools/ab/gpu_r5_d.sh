@@ -2,7 +2,7 @@
 # round 5: ESS frames with the tail-given-reference-depths check, the perturbed
 # interleaved C4 test, then a bench line
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r5_d}
 mkdir -p $O

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Run named GPU steps, each under its own time limit, logs under gpurun_out/$TAG.
-# Usage: TAG=x bash tools/gpu_steps.sh "name:timeout:command" ...
+# Usage: TAG=x bash tools/ab/gpu_steps.sh "name:timeout:command" ...
 # A crash / time limit (rc >= 124) or a signal stops the script; an ordinary
 # failure (rc 1-123) is reported and the next step runs.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-steps}
 mkdir -p "$OUT"

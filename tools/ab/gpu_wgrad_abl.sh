@@ -2,7 +2,7 @@
 # timing-only ablations of the batched weight-gradient kernel (make variant V=wabl1/2):
 # 1 = no MFMAs, 2 = no operand stream; the shipped kernel in between
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/${TAG:-wabl}
 mkdir -p $O
 for v in base wabl1 wabl2 base; do

@@ -5,7 +5,7 @@ amax + ReLU bits; backward: masked by those bits) at the C3 fine-pass size
 order) against chunk-major (every layer of a sample chunk before the next
 chunk), HIP-event medians; outputs compared bitwise.
 
-    python tools/ic_chunk_bench.py [chunk divisors ...]
+    python tools/ab/ic_chunk_bench.py [chunk divisors ...]
 
 Measured (round 2): chunking is SLOWER (8 layers fwd 1021 us at 1 chunk, 1038 /
 1069 / 1277 us at 2 / 3 / 4): no Infinity Cache gain that pays for the shorter
@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 
 

@@ -5,7 +5,7 @@
 Per-slice cost ratio = (t_train / 73) / (t_inf / 65): 1.0 means the stores are
 free.
 
-    python tools/time_train_fwd.py [P] [reps]
+    python tools/ab/time_train_fwd.py [P] [reps]
 """
 import ctypes
 import os
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 
 

@@ -4,14 +4,14 @@ P samples with the fused kernels on / off (NERF_TRAIN_FUSED_FORWARD /
 _BACKWARD as module switches), HIP events on the launch stream around each
 phase, medians over reps. The backward includes the batched weight gradients.
 
-    python tools/time_train_mlp.py [P] [reps]
+    python tools/ab/time_train_mlp.py [P] [reps]
 """
 import os
 import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 sys.path.insert(0, REPO)
 

@@ -5,14 +5,14 @@ shader cycles and the share of a tile spent before its first MFMA (sample
 inputs + encoding), over workgroups 0-3's first 32 tiles -- on the bench
 frame's coarse pass shape (800 x 800 rays x 64 depths, synthetic weights).
 
-    python tools/trace_x3.py [reps]
+    python tools/ab/trace_x3.py [reps]
 """
 import os
 import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "nerf-rep_for_test_amd"))
 
 
