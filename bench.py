@@ -55,13 +55,17 @@ DEFAULT_CKPT = os.path.join(REPO, "checkpoints", "lego")
 GT_PATH = os.path.join(REPO, "data", "lego", "test.npz")
 
 
+POSE_STRIDE = [GT_STRIDE]   # --all-poses: 1 (every one of the 200 test poses)
+
+
 def lego_camera(H, W, idx):
-    """Test view GT_STRIDE * (idx mod 25): the frames whose ground truth is packed."""
+    """Test view POSE_STRIDE * idx (mod 200): by default the frames 0, 8, ..., 192
+    whose ground truth is packed; with --all-poses every test pose in turn."""
     cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
     poses, angle = cams["poses"], float(cams["camera_angle_x"])
     focal = 0.5 * W / np.tan(0.5 * angle)            # blender.py:41-42
     K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
-    return poses[(GT_STRIDE * idx) % len(poses)], K
+    return poses[(POSE_STRIDE[0] * idx) % len(poses)], K
 
 
 def main():
@@ -81,8 +85,9 @@ def main():
                     help="c2: lego 800x800 64c+128f (BASELINE configs[1], the headline); "
                          "c3: train step, 1024 rays/rank (configs[2]); "
                          "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99); "
-                         "c5: the lego test set (the 25 packed views cycled, one per step; "
-                         "PSNR/SSIM over all of them from the sharded renders, configs[4])")
+                         "c5: the lego test set (the 25 packed views cycled, one per step, or "
+                         "with --all-poses all 200 test poses; PSNR/SSIM over the --gt-path "
+                         "views from the sharded renders, configs[4])")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 (ESS + ERT) sub-record of the default run")
     ap.add_argument("--checkpoint", default=None,
@@ -114,7 +119,15 @@ def main():
                          "Mrays/s, 16: 1.92, 32: 1.86, 64: 1.70 measured)")
     ap.add_argument("--no-fp32-run", action="store_true",
                     help="skip the second, FP32-MFMA timing reported under 'fp32_mfma'")
+    ap.add_argument("--all-poses", action="store_true",
+                    help="time every one of the 200 lego test poses in turn (c5: --steps 200 "
+                         "is the whole test split) instead of the 25 packed views")
+    ap.add_argument("--gt-path", default=GT_PATH,
+                    help="packed ground-truth views for psnr_vs_gt (tools/pack_lego.py; "
+                         "data/lego/test_all.npz: all 200 test views)")
     args = ap.parse_args()
+    if args.all_poses:
+        POSE_STRIDE[0] = 1
 
     import torch
     import torch.distributed as dist
@@ -224,8 +237,10 @@ def main():
         "vs_baseline": None,
         "dtype": DTYPES[args.precision],
         "data": data,
-        "config": {"workload": ("lego 800x800 test set (the 25 packed test views 0, 8, ..., 192 "
-                                "cycled), " if c5 else
+        "config": {"workload": (("lego 800x800 test set (all 200 test poses in turn), "
+                                 if args.all_poses else
+                                 "lego 800x800 test set (the 25 packed test views 0, 8, ..., "
+                                 "192 cycled), ") if c5 else
                                 "lego 800x800, ") + "64 coarse + 128 fine samples, 1 frame per step "
                                "(test poses cycled), " +
                                ("ESS + ERT on (threshold 0.01, synthetic occupancy grid, "
@@ -264,8 +279,8 @@ def main():
         else:
             result["parity_vs_reference_frame"] = reference_frame_parity(
                 pipe, "r0_c2_frame0", H, W, ckpt)
-    if (c5 or (world == 1 and not c4)) and not args.no_gt and os.path.exists(GT_PATH):
-        ev = testset_eval(frame_fn(pipe, c4), H, W, rank, result.get("parity"))
+    if (c5 or (world == 1 and not c4)) and not args.no_gt and os.path.exists(args.gt_path):
+        ev = testset_eval(frame_fn(pipe, c4), H, W, rank, result.get("parity"), args.gt_path)
         if rank == 0:
             result["psnr_vs_gt"] = ev
     del pipe
@@ -907,7 +922,7 @@ def _cpu_model():
     return None
 
 
-def testset_eval(frame, H, W, rank, parity):
+def testset_eval(frame, H, W, rank, parity, gt_path=GT_PATH):
     """North_star "PSNR on lego" over the test set: the evaluator's PSNR / SSIM
     (evaluators/nerf.py:465-504; nerfhip.evaluate) of the HIP render of every
     packed lego test view (data/lego/test.npz: frames 0, 8, ..., 192, rendered at
@@ -916,7 +931,7 @@ def testset_eval(frame, H, W, rank, parity):
     HIP render and for the oracle's render of those rays."""
     import torch
     from nerfhip.evaluate import load_packed, psnr, ssim
-    gts, poses, focal, frames = load_packed(GT_PATH, H, W)
+    gts, poses, focal, frames = load_packed(gt_path, H, W)
     K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
     vals, ssims = [], []
     for i, fr in enumerate(frames):
@@ -928,11 +943,12 @@ def testset_eval(frame, H, W, rank, parity):
     torch.cuda.synchronize()
     if rank != 0:
         return None
-    out = {"frames": [int(f) for f in frames], "psnr": vals, "psnr_mean": float(np.mean(vals)),
-           "ssim_mean": float(np.mean(ssims)),
+    out = {"frames": [int(f) for f in frames], "views": len(vals), "psnr": vals,
+           "psnr_mean": float(np.mean(vals)), "ssim_mean": float(np.mean(ssims)),
+           "gt": os.path.relpath(gt_path, REPO),
            "metric": "evaluators/nerf.py PSNR (clip to [0,1], -10 log10 mse) and SSIM, "
                      "mean over the packed test views"}
-    if parity and "_maps" in parity:
+    if parity and "_maps" in parity and int(frames[0]) == 0:
         g, o = parity.pop("_maps")
         r0, r1 = parity["strip_rows"]
         assert int(frames[0]) == 0

@@ -188,7 +188,29 @@ struct SplitHook {
 struct NoPend {
   template <int P>
   __device__ __forceinline__ void pair(const Op&) {}
+  template <int P, int R>
+  __device__ __forceinline__ void part(const Op&) {}
 };
+
+// NERF_STORE_SPREAD (a study build, never shipped; round 4's store-spreading
+// variant recreated for the static ISA check): the waves that stage
+// no weight pieces (4-7) spread a pair's stores over groups 0-3, two per group
+#ifndef NERF_STORE_SPREAD
+#define NERF_STORE_SPREAD 0
+#endif
+template <int P, int G, typename Pend>
+__device__ __forceinline__ void store_pair_at(Pend& st, const Op& v) {
+#if NERF_STORE_SPREAD
+  const bool loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4;
+  if (loader) {
+    if constexpr (G == 0) st.template pair<P>(v);
+  } else if constexpr (G < 4) {
+    st.template part<P, G>(v);
+  }
+#else
+  if constexpr (G == 0) st.template pair<P>(v);
+#endif
+}
 
 template <int P, typename Pend, typename Split>
 struct StoreThen {
@@ -199,7 +221,7 @@ struct StoreThen {
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
     // behind group 0's MFMAs (they issue first), ahead of the slice's pieces
-    if constexpr (G == 0) st.template pair<P>(sp.op);
+    store_pair_at<P, G>(st, sp.op);
     sp.template after<G>(acc);
   }
 };
@@ -376,14 +398,17 @@ struct Lay {
   __device__ __forceinline__ static int rowpart(int row) {   // T16, floats
     return (row >> 4) * 256 + (row & 3) * 64 + ((row >> 2) & 3) * 16;
   }
-  // element (row, p), bytes
+  // element (row, p), bytes (T: the T16 layout, a kernel's compile-time choice)
+  template <bool T>
   __device__ __forceinline__ unsigned elem(int row, int64_t p) const {
-    return bs ? (unsigned)(((p >> 4) * bs + rowpart(row) + (p & 15)) * 4)
-              : (unsigned)(((int64_t)row * ld + p) * 4);
+    if constexpr (T) return (unsigned)(((p >> 4) * bs + rowpart(row) + (p & 15)) * 4);
+    else return (unsigned)(((int64_t)row * ld + p) * 4);
   }
   // bytes an output of `rows` rows spans from its pointer (its num_records)
+  template <bool T>
   __device__ __forceinline__ int extent(int rows) const {
-    return bs ? (int)(((nblk - 1) * bs + ((rows + 15) & ~15) * 16) * 4) : (int)((int64_t)rows * ld * 4);
+    if constexpr (T) return (int)(((nblk - 1) * bs + ((rows + 15) & ~15) * 16) * 4);
+    else return (int)((int64_t)rows * ld * 4);
   }
 };
 
@@ -397,8 +422,9 @@ struct ActStore {
   unsigned wb;                 // bits of the current 4-tile block
   bool bits, valid;
   bool on = true;              // uniform: false = these rows are not stored (null output)
+  template <bool T>
   __device__ __forceinline__ void set_lay(const Lay& L, int64_t tile, int wave) {
-    if (L.bs) {
+    if constexpr (T) {
       soff = (unsigned)((tile * 8 + wave) * L.bs * 4);
       c4 = 64u; ts = 1024u; rstr = 256u;
     } else {
@@ -411,6 +437,34 @@ struct ActStore {
     unsigned lid = __lane_id();
     asm volatile("" : "+v"(lid));
     return valid ? (lid >> 4) * c4 + (lid & 15u) * 4u + soff : 0x7fffffffu;
+  }
+  // (NERF_STORE_SPREAD study builds) element R of pair G's two tiles; the bits
+  // of the pair with its last element
+  template <int G, int R>
+  __device__ __forceinline__ void part(const Op& v) {
+    if (!on) return;
+    const unsigned vo = lane_off();
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[R]), rs, (int)vo,
+                                          (int)(2 * G * ts + R * rstr), NERF_ACT_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + R]), rs, (int)vo,
+                                          (int)((2 * G + 1) * ts + R * rstr), NERF_ACT_STORE_AUX);
+    if constexpr (R == 3) store_bits<G>(v);
+  }
+  template <int G>
+  __device__ __forceinline__ void store_bits(const Op& v) {
+    if (bits) {   // bit 4t + r of the block word = (h > 0): post-ReLU h >= 0
+      unsigned m = 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m |= min(__float_as_uint(v[j]), 1u) << j;
+      if constexpr ((G & 1) == 0) {
+        wb = m;
+      } else {
+        wb |= m << 8;
+        if (valid)
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)wb, rb, (int)(__lane_id() * 2u),
+                                                (int)(sboff + (G >> 1) * 128), 0);
+      }
+    }
   }
   // pair G = tiles 2G (v[0..3], rows 32G + 4 g4 + r) and 2G+1 (v[4..7], rows + 16).
   // The lane's offsets are recomputed here (a few VALU in the MFMA shadows)
@@ -427,19 +481,7 @@ struct ActStore {
                                             (int)((2 * G + 1) * ts + r * rstr),
                                             NERF_ACT_STORE_AUX);
     }
-    if (bits) {   // bit 4t + r of the block word = (h > 0): post-ReLU h >= 0
-      unsigned m = 0u;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m |= min(__float_as_uint(v[j]), 1u) << j;
-      if constexpr ((G & 1) == 0) {
-        wb = m;
-      } else {
-        wb |= m << 8;
-        if (valid)
-          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)wb, rb, (int)(__lane_id() * 2u),
-                                                (int)(sboff + (G >> 1) * 128), 0);
-      }
-    }
+    store_bits<G>(v);
   }
 };
 
@@ -475,8 +517,10 @@ __device__ __forceinline__ int enc_dir_row(int g, int j) {
 // is enforced by the launchers: the sum cannot wrap), and a null output (the
 // skipped feature / DF rows) gets num_records 0: every store through it is
 // dropped even if a path forgets the ActStore::on test.
+template <bool T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, const Lay& L) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, p ? L.extent(rows) : 0, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, p ? L.template extent<T>(rows) : 0,
+                                           0x00020000);
 }
 
 // LIST: the samples are the flat indices list[0 .. *count) (ray * S + step,
@@ -487,7 +531,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* p, int rows, 
 // s_memtime at each of its first 32 tiles' start, after the tile's sample
 // loads + encoding, and at its end: trace[(b * 32 + i) * 4 + 0..2]; [3]: after
 // the loads, before the encoding.
-template <bool LIST, bool TRAIN, bool TRACE = false>
+template <bool LIST, bool TRAIN, bool TRACE = false, bool T16 = false>
 __device__ __forceinline__ void mlp_x3_body(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
@@ -557,12 +601,13 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the encoding rows (the wgrad operand of layers 0 and 5)
     int i10 = 10;
     asm volatile("" : "+s"(i10));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i10], 64, to.lay);
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc<T16>(to.act[i10], 64, to.lay);
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const unsigned vo = valid ? to.lay.elem(enc_xyz_row(g4, q, j), gs) : 0x7fffffffu;
+        const unsigned vo = valid ? to.lay.template elem<T16>(enc_xyz_row(g4, q, j), gs)
+                                  : 0x7fffffffu;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(encf[q][j]), rs, (int)vo, 0, 0);
       }
   }
@@ -580,12 +625,12 @@ __device__ __forceinline__ void mlp_x3_body(
       // pointers would not fit the SGPR budget)
       int Li = L;
       asm volatile("" : "+s"(Li));
-      st.rs = rows_rsrc(to.act[Li], rows, to.lay);
+      st.rs = rows_rsrc<T16>(to.act[Li], rows, to.lay);
       st.on = to.act[Li] != nullptr;   // the feature rows may be skipped (act[8] null)
       st.bits = L < 8;
       st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)to.bits[Li < 8 ? Li : 0], 0,
                                                 L < 8 ? 0x7fffffff : 0, 0x00020000);
-      st.set_lay(to.lay, tile, wv);
+      st.template set_lay<T16>(to.lay, tile, wv);
       st.sboff = (unsigned)(((tile * 8 + wv) * 4) * 64 * 2);
       st.wb = 0u;
       st.valid = valid;
@@ -693,10 +738,10 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the view-encoding rows (the views layer's wgrad operand)
     int i11 = 11;
     asm volatile("" : "+s"(i11));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i11], 32, to.lay);
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc<T16>(to.act[i11], 32, to.lay);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const unsigned vo = valid ? to.lay.elem(enc_dir_row(g4, j), gs) : 0x7fffffffu;
+      const unsigned vo = valid ? to.lay.template elem<T16>(enc_dir_row(g4, j), gs) : 0x7fffffffu;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dirf[j]), rs, (int)vo, 0, 0);
     }
     amax_to_lds(10, op_absmax(dirf));
@@ -737,10 +782,10 @@ __device__ __forceinline__ void mlp_x3_body(
   if constexpr (TRAIN) {   // the views output rows, its ReLU bits (MT 8) and max
     int i9 = 9;
     asm volatile("" : "+s"(i9));
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(to.act[i9], 128, to.lay);
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc<T16>(to.act[i9], 128, to.lay);
     ActStore sv;
     sv.valid = valid;
-    sv.set_lay(to.lay, tile, wave);
+    sv.template set_lay<T16>(to.lay, tile, wave);
     const unsigned voff = sv.lane_off();
     float vmax = 0.0f;
 #pragma unroll
@@ -829,12 +874,13 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_clock_kernel(
 // The training forward: sample p = ray * S + step at o + d * z (VR:165) as the
 // inference kernel (nerf_mlp_train_forward_x3 passes rays_o = pts, rays_d =
 // dirs, one shared zero depth and S = 1: o + d * 0 = o).
+template <bool T16>
 __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_train_kernel(
     const float4* __restrict__ slices, const float* __restrict__ head,
     const float* __restrict__ rays_o, const float* __restrict__ rays_d,
     const float* __restrict__ z, int64_t z_stride, int64_t total, int S,
     float4* __restrict__ raw, const X3TrainOut to) {
-  mlp_x3_body<false, true>(slices, head, rays_o, rays_d, z, z_stride, total, S, raw, nullptr,
+  mlp_x3_body<false, true, false, T16>(slices, head, rays_o, rays_d, z, z_stride, total, S, raw, nullptr,
                            nullptr, to);
 }
 
@@ -958,7 +1004,7 @@ struct StoreMaskThen {
   }
   template <int G, typename Acc>
   __device__ __forceinline__ void after(Acc& acc) {
-    if constexpr (G == 0 && P >= 0) st.template pair<P>(sp.op);   // behind group 0's MFMAs
+    if constexpr (P >= 0) store_pair_at<P, G>(st, sp.op);   // behind group 0's MFMAs
     sp.template after<G>(acc);
     if constexpr (G == 7) {
       if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1001,7 +1047,7 @@ __device__ __forceinline__ void dgrad_slices(f32x4 (&acc)[16], const Ring& R, in
   epi.finish(acc);
 }
 
-template <bool ENC>
+template <bool ENC, bool T16>
 __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     const float4* __restrict__ slices, const float* __restrict__ head, int64_t P,
     const X3BwdIO io) {
@@ -1038,20 +1084,20 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (io.d_raw_t && g4 == 0 && valid) {   // d raw as 4 rows: the heads' wgrad operands
     char* t = reinterpret_cast<char*>(io.d_raw_t);
-    *reinterpret_cast<float*>(t + io.lay.elem(0, gs)) = dr.w;
-    *reinterpret_cast<float*>(t + io.lay.elem(1, gs)) = dr.x;
-    *reinterpret_cast<float*>(t + io.lay.elem(2, gs)) = dr.y;
-    *reinterpret_cast<float*>(t + io.lay.elem(3, gs)) = dr.z;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(0, gs)) = dr.w;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(1, gs)) = dr.x;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(2, gs)) = dr.y;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(3, gs)) = dr.z;
   }
   // outputs / masks of this (tile, wave): pointers loaded at their layer
   auto store_for = [&](int k, int rows) {
     ActStore st;
     int ki = k;
     asm volatile("" : "+s"(ki));
-    st.rs = rows_rsrc(io.d[ki], rows, io.lay);
+    st.rs = rows_rsrc<T16>(io.d[ki], rows, io.lay);
     st.on = io.d[ki] != nullptr;       // DF may be skipped (d[8] null)
     st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
-    st.set_lay(io.lay, tile, wave);
+    st.template set_lay<T16>(io.lay, tile, wave);
     st.sboff = 0u;
     st.wb = 0u;
     st.bits = false;
@@ -2190,9 +2236,14 @@ extern "C" int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float
   for (int i = 0; i < 9; ++i) to.bits[i] = out->bits[i];
   to.amax = out->amax;
   to.lay = make_lay(out->ld, out->bs, P);
-  hipLaunchKernelGGL(mlp_x3_train_kernel, dim3((unsigned)grid), dim3(kX3Threads), 0,
-                     as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
-                     z_stride, P, S, (float4*)raw, to);
+  if (out->bs)
+    hipLaunchKernelGGL(mlp_x3_train_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                       as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
+                       z_stride, P, S, (float4*)raw, to);
+  else
+    hipLaunchKernelGGL(mlp_x3_train_kernel<false>, dim3((unsigned)grid), dim3(kX3Threads), 0,
+                       as_stream(stream), (const float4*)w_slices, w_head, rays_o, rays_d, z,
+                       z_stride, P, S, (float4*)raw, to);
   return check_launch("mlp_x3_train_kernel");
 }
 
@@ -2224,12 +2275,10 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
   b.dmax = io->dmax;
   b.lay = make_lay(io->ld, io->bs, P);
   b.d_raw_t = io->d_raw_t;
-  if (with_enc)
-    hipLaunchKernelGGL(mlp_x3_bwd_kernel<true>, dim3((unsigned)grid), dim3(kX3Threads), 0,
-                       as_stream(stream), (const float4*)w_slices, w_head, P, b);
-  else
-    hipLaunchKernelGGL(mlp_x3_bwd_kernel<false>, dim3((unsigned)grid), dim3(kX3Threads), 0,
-                       as_stream(stream), (const float4*)w_slices, w_head, P, b);
+  auto* k = with_enc ? (io->bs ? mlp_x3_bwd_kernel<true, true> : mlp_x3_bwd_kernel<true, false>)
+                     : (io->bs ? mlp_x3_bwd_kernel<false, true> : mlp_x3_bwd_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kX3Threads), 0, as_stream(stream),
+                     (const float4*)w_slices, w_head, P, b);
   return check_launch("mlp_x3_bwd_kernel");
 }
 

@@ -6,6 +6,12 @@ when the asm issues. If it reuses one before the drain (e.g. because it deleted
 a consumer MFMA whose result it proved dead), the late LDS data clobbers a live
 value -- an address, in the fault that motivated this test. Also pins the MFMA
 count (no slice's work folded away) and zero scratch.
+
+Round 5: the checker walked the control-flow graph from the file's first
+block only, i.e. it checked the first kernel of each .s (mlp_x3_clock_kernel,
+mlp_fused_kernel) and none of the others; it now starts from every kernel's
+entry, so the inference, training, backward, weight-gradient and layer kernels
+are all held to it (tools/check_async_lds.py).
 """
 import os
 import re

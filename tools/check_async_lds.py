@@ -1,7 +1,8 @@
 """Static check of the inline-asm asynchronous LDS reads in a kernel's ISA.
 
-The fused MLP kernels issue ds_read_b128 through inline asm and wait for them
-explicitly (s_waitcnt lgkmcnt(0)); the compiler believes the destination
+The fused MLP kernels issue ds_read_* (b128 fragments, u16 mask words) through
+inline asm and wait for them explicitly (s_waitcnt lgkmcnt(0)); every kernel
+of the file is checked. The compiler believes the destination
 registers are written when the asm issues. This script flags any instruction
 between such a read and its drain that reads or writes one of the pending
 destination VGPRs or AGPRs (a stale read, or a register the late data would
@@ -99,11 +100,11 @@ def _run_block(ins, s, e, pending, report):
         used = set()
         for o in ops:
             used |= regs(o.split()[0] if o else "")
-        if in_asm and op == "ds_read_b128":
+        if in_asm and op.startswith("ds_read"):
+            # another asm read into a pending register is harmless (LDS returns in
+            # order: the later read's data land last), e.g. a fragment group the
+            # compiler found dead re-using one destination; any other access is not
             dst = regs(ops[0])
-            clash = dst & set(pending)
-            if clash:
-                report(line, f"asm read overwrites pending regs {sorted(clash)}")
             for r in dst:
                 pending[r] = line + 1
             continue
@@ -122,8 +123,13 @@ def main(path):
     bounds, succ = _blocks(ins, labels)
     entry = [dict() for _ in bounds]
     seen = [False] * len(bounds)
-    seen[0] = True
-    work = [0]
+    # every kernel of the file: each function symbol's block is an entry (a
+    # walk from block 0 alone only reaches the first kernel)
+    at = {s: k for k, (s, _) in enumerate(bounds)}
+    work = sorted({0} | {at[p] for name, p in labels.items()
+                         if not name.startswith(".") and p in at})
+    for k in work:
+        seen[k] = True
     while work:                                 # forward dataflow to a fixpoint
         k = work.pop()
         out = _run_block(ins, *bounds[k], entry[k], lambda *a: None)

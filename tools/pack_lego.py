@@ -9,6 +9,8 @@ pixels) together with the camera poses of ``transforms_<split>.json``:
 
   data/lego/train.npz  100 train views (BASELINE configs[2] training data)
   data/lego/test.npz   every 8th test view (frames 0, 8, ..., 192): the PSNR set
+  data/lego/test_all.npz  all 200 test views (--splits test --test-stride 1: the
+                       whole test split for bench.py --config c5 --gt-path)
 
 Keys: ``png_bytes`` uint8 (concatenated files), ``png_offsets`` int64 [N+1],
 ``frames`` int32 [N] (index into the split's json), ``poses`` float32 [N,4,4],
@@ -48,10 +50,15 @@ def main(argv=None):
     ap.add_argument("--src", default=SRC)
     ap.add_argument("--out", default=os.path.join(REPO, "data", "lego"))
     ap.add_argument("--splits", default="train,test")
+    ap.add_argument("--test-stride", type=int, default=8,
+                    help="every n-th test view (8: the 25-view PSNR set test.npz; 1: all 200 "
+                         "views, written as test_all.npz for bench.py --config c5 --gt-path)")
     args = ap.parse_args(argv)
     os.makedirs(args.out, exist_ok=True)
     for split in args.splits.split(","):
-        pack(args.src, split, 8 if split == "test" else 1, os.path.join(args.out, f"{split}.npz"))
+        stride = args.test_stride if split == "test" else 1
+        name = "test_all" if split == "test" and stride == 1 else split
+        pack(args.src, split, stride, os.path.join(args.out, f"{name}.npz"))
 
 
 if __name__ == "__main__":
