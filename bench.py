@@ -191,6 +191,8 @@ def main():
     def frame_fn(pipe, ess_ert, perturb=False):
         return make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb)
 
+    shard_stats = {}
+
     def measure(precision, ess_ert, steps, warmup, perturb=False):
         """warmup + K timed frames (barrier + sync both sides, max over ranks)."""
         pipe = make_pipe(precision, ess_ert)
@@ -199,6 +201,7 @@ def main():
             frame(*lego_camera(H, W, i))
         torch.cuda.synchronize()
         barrier()
+        pipe.replayed_chunks = 0
         pipe.timer = []
         pipe.stage_timer = []
         pipe.ert_stats = []
@@ -215,6 +218,8 @@ def main():
             elapsed = float(t.item())
         timer, pipe.timer = pipe.timer, None
         stages, pipe.stage_timer = pipe.stage_timer, None
+        shard_stats[(ess_ert, perturb)] = shard_report(pipe, timer, steps, H, W, rank, world,
+                                                       ess_ert)
         roof = roofline(precision, timer, elapsed, world, H, W,
                         pmc_workload=world == 1 and not ess_ert and not perturb)
         roof["byte_kernels"] = byte_kernels(stages, steps)
@@ -257,6 +262,8 @@ def main():
     }
     if c4:
         result["ert_compaction"] = ert_report(pipe, rays, world, args.ert_segment, dev)
+    if world > 1 and rank == 0:
+        result["shards"] = shard_stats[(c4, False)]
     cpu = host_cpus()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.set_num_threads(cpu["threads_used"])
@@ -816,6 +823,33 @@ def host_cpus():
     return {"cpu_model": _cpu_model(), "logical_cpus": logical, "sockets": len(sockets) or None,
             "physical_cores": physical, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
             "threads_used": max(1, use)}
+
+
+def shard_report(pipe, timer, steps, H, W, rank, world, ess_ert):
+    """Per-rank work of the sharded frame (gathered to rank 0; None elsewhere):
+    owned pixels / chunks, foreign grid-update chunks replayed (C4: every rank
+    replays the reference's updating chunks it does not own, VR:1147-1157), and
+    the MLP launches with their sample counts, per frame."""
+    import torch.distributed as dist
+    from nerfhip.dist import band, chunk_set
+    if ess_ert:
+        mine, n, _ = chunk_set(H, W, rank, world)
+        owned = {"chunks": len(mine), "pixels": n}
+    else:
+        p0, n, _ = band(H, W, rank, world)
+        owned = {"pixels": n}
+    sizes = [int(t[2]) for t in (timer or [])]   # (ERT list launches: a device count)
+    rec = {"rank": rank, **owned,
+           "replayed_chunks_per_frame": pipe.replayed_chunks / max(1, steps),
+           "mlp_launches_per_frame": len(sizes) / max(1, steps),
+           "mlp_samples_per_launch_mean": float(np.mean(sizes)) if sizes else 0.0,
+           "mlp_samples_per_launch_min": int(min(sizes)) if sizes else 0,
+           "mlp_samples_per_launch_max": int(max(sizes)) if sizes else 0}
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out if rank == 0 else None
 
 
 def ert_report(pipe, rays, world, segment, dev):

@@ -100,6 +100,7 @@ class NerfPipeline:
         self.stage_timer = None   # list -> (kernel, start event, end event, algorithmic bytes)
         self.capture_zall = None  # list -> the merged fine depths [m, S+NI] of every pass (tests)
         self._replaying = False   # replays of foreign update chunks: not in ert_stats
+        self.replayed_chunks = 0  # foreign update chunks replayed (multi-GPU C4 overhead)
         self._updates_on = True   # render_chunks switches the grid self-update off for blocks
                                   # of non-consecutive chunks that hold no updating chunk
 
@@ -420,6 +421,7 @@ class NerfPipeline:
         """Run a replay of a foreign chunk (its grid update only; its samples are
         not this rank's and stay out of ert_stats)."""
         self._replaying = True
+        self.replayed_chunks += 1
         try:
             return fn()
         finally:
