@@ -324,7 +324,8 @@ typedef struct NerfX3BwdIO {
   float* d[12];
   float* dmax;
   int64_t ld;
-  float* d_raw_t;   /* nullable: d raw feature-major, rows (stride ld) d sigma, d r, d g, d b */
+  float* d_raw_t;   /* nullable: d raw as rows: d sigma at row 0, d r, d g, d b at rows 1..3
+                       (feature-major, stride ld) or 16..18 (T16: a 16-row group of their own) */
   int64_t bs;       /* as NerfX3TrainOut.bs (ABI 3) */
 } NerfX3BwdIO;
 /* nerf_mlp_forward_x3_clock: nerf_mlp_forward_x3's computation (same outputs)

@@ -812,13 +812,14 @@ T16 = _os.environ.get("NERF_TRAIN_T16", "1") != "0"
 _FWD_ROWS = {"E": (0, 320), "V": (320, 608), "HV": (608, 736)}
 _FWD_H = {0: 736, 1: 992, 2: 1248, 3: 1504, 5: 1760, 6: 2016}
 _FWD_R = 2272
-# the fused backward's rows: [d_hv 128 | d raw 4] (hx), D0..D7, d_enc5, d_enc0
-_BWD_HX, _BWD_D, _BWD_E5, _BWD_E0, _BWD_R = 0, 144, 2192, 2256, 2320
+# the fused backward's rows: hx = [d_hv 128 | d sigma, 15 spare | d rgb 3, 13 spare]
+# (every wgrad operand starts a 16-row group), D0..D7, d_enc5, d_enc0
+_BWD_HX, _BWD_D, _BWD_E5, _BWD_E0, _BWD_R = 0, 160, 2208, 2272, 2336
 
 
 def _t16_ok(P):
     """T16 for a pass of P samples: the larger (backward) buffer within the 2 GiB
-    of the kernels' 32-bit buffer offsets (P <= 229 376: a 1024-ray C3 step's
+    of the kernels' 32-bit buffer offsets (P <= 229 760: a 1024-ray C3 step's
     fine pass is 196 608; larger passes stay feature-major)."""
     return T16 and 0 < P and -(-P // 128) * 128 * _BWD_R * 4 < (1 << 31)
 
@@ -992,8 +993,9 @@ class NerfMLPFn(torch.autograd.Function):
         heads_merged = ctx.fused_backward and v_h7
         bbuf = BlockRows.alloc(_BWD_R, P, dev) if t16 else None   # the backward's rows
         if heads_merged:
-            HX = bbuf.rows(_BWD_HX, _BWD_HX + 132) if t16 else _act(132, P, dev)
-            d_sig, d_rgb = rows_of(HX, 128, 129), rows_of(HX, 129, 132)
+            HX = bbuf.rows(_BWD_HX, _BWD_HX + 160) if t16 else _act(132, P, dev)
+            d_sig = rows_of(HX, 128, 129)
+            d_rgb = rows_of(HX, 144, 147) if t16 else HX[129:132]
         else:
             # d_raw^T (the rgb / alpha heads' wgrad operands; the layer launches'
             # d hv K step: 32 rows, 4 of them d_raw)
