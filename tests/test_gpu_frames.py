@@ -30,13 +30,24 @@ held to:
   the attributed sampling flips), and
   PSNR(HIP vs reference) >= 60 dB;
 * C4 (ESS + ERT): the final occupancy grid bit for bit and the call counter
-  after the reference's in-frame grid self-updates (VR:1147-1155).
+  after the reference's in-frame grid self-updates (VR:1147-1155);
+* every tail pixel once more on the reference's OWN fine depths (round 5,
+  _tail_given_reference_depths): the pixel must be in the captured set
+  (tests/golden/zt_<frame>.npz, make_ref_frames.py --tail: the reference's coarse
+  depths and weights of the pixels near or beyond tolerance), the oracle's
+  sample_fine + merge of the reference's coarse weights must reproduce the
+  reference's fine-row hash (tail_oracle_hash_mismatch == 0), and the HIP fine
+  MLP + composite (ERT: each chunk's decision restored, VR:1116) on exactly those
+  rows must give the reference's maps within tolerance (max ratio <= 1), save
+  for rays whose own ERT cut sits within 1e-4 of the threshold by the oracle's
+  transmittance (counted, at most 5 per frame).
 
 r0 runs through NerfPipeline (the bench path); r1 through the drop-in plugin
 ``Renderer(net).render(batch)`` with the reference's perturb draws replayed
 from torch's CPU generator (seeded as the capture was, one [m, 64] draw per
 2048-ray chunk); r2 is C4 (f16x3: the bench's compacted-ERT path; fp32: full
-evaluation). With NERF_FRAME_REPORT=<dir> each case writes its numbers to
+evaluation); r3 is lego.yaml's own eval configuration through the plugin
+(ESS + ERT + perturb 1, the Renderer's own grid drawn at construction). With NERF_FRAME_REPORT=<dir> each case writes its numbers to
 <dir>/frame_parity_<name>_<prec>.json.
 """
 import json
