@@ -1367,7 +1367,10 @@ __device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n un
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
     case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
@@ -1771,6 +1774,9 @@ constexpr int kWgRing = 5;
 #ifndef NERF_WGRAD_ABL
 #define NERF_WGRAD_ABL 0
 #endif
+#ifndef NERF_WGRAD_SELFSPLIT   // 0: every wave splits the fragments it reads (round 4)
+#define NERF_WGRAD_SELFSPLIT 1
+#endif
 __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
@@ -1843,7 +1849,6 @@ __device__ __forceinline__ void wgrad_dma_body(
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.0f);
-  float rs4[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's share of sum_p A (nb = 0)
 
   // the raw FP32 fragment of a tile: its two pieces (halves), 1 KiB apart
   // Raw: the two halves as the asm wrote them. A drain names every pending Raw
@@ -1853,10 +1858,131 @@ __device__ __forceinline__ void wgrad_dma_body(
     asm volatile("ds_read_b128 %0, %1" : "=v"(r.x) : "v"(addr) : "memory");
     asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(r.y) : "v"(addr) : "memory");
   };
+
+#if NERF_WGRAD_SELFSPLIT
+  // Self split: a wave splits, in place, the fragments of the pieces it issued
+  // itself (granule g, tiles 2 wave + t, both halves), once its own vmcnt says
+  // they landed -- no barrier between the landing and the split. Half 0 then
+  // holds the FP16 hi pairs, half 1 the lo pairs, so the MFMA loop's read_pair
+  // yields (hi, lo) with no split of its own: every element is split once, not
+  // once per wave that multiplies it (A twice, B four times). Operands and
+  // their MFMA order are unchanged (bit-identical partials). A granules add
+  // their raw values to rs (the bias sums: tile 2 wave + t, this lane's row and
+  // 8 samples, in the same order as the fragment reads did).
+  float rs[2] = {0.0f, 0.0f};
+  auto split_own = [&](int g, int t, float s, bool sum) {
+    u32x4* q = reinterpret_cast<u32x4*>(&ring[g % kWgRing][(2 * (2 * wave + t)) * 64 + lane]);
+    const u32x4 x = q[0], y = q[64];
+    Op v = __builtin_bit_cast(Op, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+    if (sum) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rs[t] += v[u];
+    }
+    split_op(v, s);
+    q[0] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 0, 1, 2, 3));
+    q[64] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+  };
+
+  // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1), then this wave's share of step 0
+  for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
+  if (nsteps > 0) {
+    vm_wait_n(nsteps > 1 ? 12 : 4);   // A_0 landed
+    split_own(0, 0, sa, true);
+    split_own(0, 1, sa, true);
+    vm_wait_n(nsteps > 1 ? 8 : 0);    // B_0 landed
+    split_own(1, 0, sb, false);
+    split_own(1, 1, sb, false);
+  }
+  for (int k = 0; k < nsteps; ++k) {
+    // step k's fragments were split by their owners (the prologue or step k - 1)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every split visible; B_{k-1}'s slot is free
+    asm volatile("" ::: "memory");
+    // A_{k+2} into B_{k-1}'s slot from the start of the step; B_{k+2} into A_k's
+    // slot after the mid-step barrier (every wave holds its A_k fragments). This
+    // wave splits its share of A_{k+1} at B tiles 4-5 and of B_{k+1} at 6-7: A
+    // lands in 1.5 steps, B in about 1.25.
+    const int ga = 2 * k + 4, gb = 2 * k + 5;
+    const bool nxt = k + 1 < nsteps, nxt2 = k + 2 < nsteps;
+    if (!busy) {   // nothing to multiply: stage and split this wave's pieces
+      issue(ga);
+      __builtin_amdgcn_s_barrier();
+      if (nxt) {
+        vm_wait_n(nxt2 ? 8 : 4);
+        split_own(2 * k + 2, 0, sa, true);
+        split_own(2 * k + 2, 1, sa, true);
+      }
+      issue(gb);
+      if (nxt) {
+        vm_wait_n(nxt2 ? 8 : 0);
+        split_own(2 * k + 3, 0, sb, false);
+        split_own(2 * k + 3, 1, sb, false);
+      }
+      continue;
+    }
+    const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
+    const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
+    Raw ra[4], rb[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
+    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);   // B tile nt = 8 nb + j
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
+                   "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y),
+                   "+v"(rb[0].x), "+v"(rb[0].y)
+                 :
+                 : "memory");
+    auto tile = [&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      Raw& cur = rb[j & 1];
+      if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
+      const half8 bh = __builtin_bit_cast(half8, cur.x), bl = __builtin_bit_cast(half8, cur.y);
+      if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
+      if constexpr (j == 4) __builtin_amdgcn_s_barrier();
+      if constexpr (j < 4) issue_piece(ga, std::integral_constant<int, j>{});
+      else issue_piece(gb, std::integral_constant<int, j - 4>{});
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const half8 ah = __builtin_bit_cast(half8, ra[i].x), al = __builtin_bit_cast(half8, ra[i].y);
+#if NERF_WGRAD_ABL == 1   // timing-only ablation: no MFMAs (operands kept live)
+        asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
+#else
+        acc[i][j] = MFMA16(ah, bh, acc[i][j]);
+        acc[i][j] = MFMA16(ah, bl, acc[i][j]);
+        acc[i][j] = MFMA16(al, bh, acc[i][j]);
+#endif
+      }
+      if (nxt) {   // after B_{k+2} piece j - 4: A_{k+1} needs 9 (4) newer in flight, B_{k+1} 7 (0)
+        if constexpr (j == 4) vm_wait_n(nxt2 ? 9 : 4);
+        if constexpr (j == 6) vm_wait_n(nxt2 ? 7 : 0);
+        if constexpr (j == 4 || j == 5) split_own(2 * k + 2, j - 4, sa, true);
+        if constexpr (j == 6 || j == 7) split_own(2 * k + 3, j - 6, sb, false);
+      }
+    };
+    tile(std::integral_constant<int, 0>{});
+    tile(std::integral_constant<int, 1>{});
+    tile(std::integral_constant<int, 2>{});
+    tile(std::integral_constant<int, 3>{});
+    tile(std::integral_constant<int, 4>{});
+    tile(std::integral_constant<int, 5>{});
+    tile(std::integral_constant<int, 6>{});
+    tile(std::integral_constant<int, 7>{});
+  }
+  if (bias_part && ntile == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {   // row 16 (2 wave + t) + (l & 15): lanes l, l^16, l^32, l^48
+      float r = rs[t];
+      r += __shfl_xor(r, 16);
+      r += __shfl_xor(r, 32);
+      const int row = m0 + 16 * (2 * wave + t) + lane;
+      if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
+    }
+  }
+#else
+  float rs4[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's share of sum_p A (nb = 0)
   auto to_op = [](const Raw& r) {
     return __builtin_bit_cast(Op, __builtin_shufflevector(r.x, r.y, 0, 1, 2, 3, 4, 5, 6, 7));
   };
-
   // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1)
   for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
   for (int k = 0; k < nsteps; ++k) {
@@ -1946,6 +2072,7 @@ __device__ __forceinline__ void wgrad_dma_body(
       if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
     }
   }
+#endif
   if (!busy) return;
   const float inv = ldexpf(1.0f, -(ea + eb));
   float* out = part + (int64_t)z * ldpart;

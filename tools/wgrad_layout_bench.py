@@ -5,6 +5,7 @@ train_mlp.BlockRows): results compared bit for bit, HIP-event times
 interleaved.
 
     python tools/wgrad_layout_bench.py [P]
+    WGRAD_DUMP=out.pt python tools/wgrad_layout_bench.py   # also save the results
 """
 import os
 import sys
@@ -43,6 +44,9 @@ def main():
         b = b if isinstance(b, tuple) else (b,)
         assert all(torch.equal(x, y) for x, y in zip(a, b)), "layouts differ"
     print("bitwise equal", flush=True)
+    if os.environ.get("WGRAD_DUMP"):   # for bit-for-bit A/B of two library builds
+        flat = [x.cpu() for r in r1 for x in (r if isinstance(r, tuple) else (r,))]
+        torch.save(flat, os.environ["WGRAD_DUMP"])
     nbytes = sum((M + N) * P * 4 for M, N, _ in shapes)
     flop = sum(2 * M * N * P for M, N, _ in shapes)
     ts = {False: [], True: []}
@@ -59,7 +63,7 @@ def main():
         t.sort()
         ms = t[len(t) // 2]
         print(f"{'block layout ' if blocked else 'feature-major'}: {ms * 1e3:7.1f} us  "
-              f"{nbytes / ms / 1e9:7.1f} GB/s (operand bytes)  "
+              f"{nbytes / ms / 1e9:7.1f} TB/s (operand bytes)  "
               f"{3 * flop / ms / 1e9:7.1f} TF (x3 executed)", flush=True)
 
 
