@@ -198,6 +198,9 @@ struct NoPend {
 #ifndef NERF_STORE_SPREAD
 #define NERF_STORE_SPREAD 0
 #endif
+#ifndef NERF_ABL_NOSTORE
+#define NERF_ABL_NOSTORE 0
+#endif
 template <int P, int G, typename Pend>
 __device__ __forceinline__ void store_pair_at(Pend& st, const Op& v) {
 #if NERF_STORE_SPREAD
@@ -472,6 +475,10 @@ struct ActStore {
   template <int G>
   __device__ __forceinline__ void pair(const Op& v) {
     if (!on) return;
+#if NERF_ABL_NOSTORE   // timing-only ablation build: no row / bit stores (wrong results)
+    asm volatile("" ::"v"(v));
+    return;
+#endif
     const unsigned vo = lane_off();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1367,9 +1374,11 @@ __device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n un
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
@@ -1774,6 +1783,12 @@ constexpr int kWgRing = 5;
 #ifndef NERF_WGRAD_ABL
 #define NERF_WGRAD_ABL 0
 #endif
+#ifndef NERF_WGRAD_EARLY   // (study builds) counted drains of the step's first reads
+#define NERF_WGRAD_EARLY 0
+#endif
+#ifndef NERF_WGRAD_SPLITPOS   // (study builds) where the next step's split runs
+#define NERF_WGRAD_SPLITPOS 0
+#endif
 #ifndef NERF_WGRAD_SELFSPLIT   // 0: every wave splits the fragments it reads (round 4)
 #define NERF_WGRAD_SELFSPLIT 1
 #endif
@@ -1923,6 +1938,14 @@ __device__ __forceinline__ void wgrad_dma_body(
     const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
     const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
     Raw ra[4], rb[2];
+#if NERF_WGRAD_EARLY
+    // A fragment 0 and B tile 0 first: tile 0's products of A fragment i start
+    // as soon as its reads are in (counted drains below), not after all ten
+    read_pair(baseA + (unsigned)((4 * mb) * 2048), ra[0]);
+    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);   // B tile nt = 8 nb + j
+#pragma unroll
+    for (int i = 1; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
     read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);   // B tile nt = 8 nb + j
@@ -1932,10 +1955,15 @@ __device__ __forceinline__ void wgrad_dma_body(
                    "+v"(rb[0].x), "+v"(rb[0].y)
                  :
                  : "memory");
+#endif
     auto tile = [&](auto Jc) {
       constexpr int j = decltype(Jc)::value;
       Raw& cur = rb[j & 1];
       if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
+#if NERF_WGRAD_EARLY   // A fragment 0 and B tile 0 in; A fragments 1-3 (6 reads) may be in flight
+      if constexpr (j == 0)
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(cur.x), "+v"(cur.y) : : "memory");
+#endif
       const half8 bh = __builtin_bit_cast(half8, cur.x), bl = __builtin_bit_cast(half8, cur.y);
       if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
       if constexpr (j == 4) __builtin_amdgcn_s_barrier();
@@ -1943,6 +1971,19 @@ __device__ __forceinline__ void wgrad_dma_body(
       else issue_piece(gb, std::integral_constant<int, j - 4>{});
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#if NERF_WGRAD_EARLY
+        if constexpr (j == 0) {   // in flight behind A fragment i: the later ones and B tile 1
+          if (i == 0)
+            ;
+          else if (i == 1)
+            asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(ra[1].x), "+v"(ra[1].y) : : "memory");
+          else if (i == 2)
+            asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(ra[2].x), "+v"(ra[2].y) : : "memory");
+          else
+            asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ra[3].x), "+v"(ra[3].y) : : "memory");
+          __builtin_amdgcn_sched_barrier(0);   // keep each drain right before its products
+        }
+#endif
         const half8 ah = __builtin_bit_cast(half8, ra[i].x), al = __builtin_bit_cast(half8, ra[i].y);
 #if NERF_WGRAD_ABL == 1   // timing-only ablation: no MFMAs (operands kept live)
         asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
@@ -1951,12 +1992,27 @@ __device__ __forceinline__ void wgrad_dma_body(
         acc[i][j] = MFMA16(ah, bl, acc[i][j]);
         acc[i][j] = MFMA16(al, bh, acc[i][j]);
 #endif
+#if NERF_WGRAD_EARLY
+        if constexpr (j == 0) __builtin_amdgcn_sched_barrier(0);
+#endif
       }
       if (nxt) {   // after B_{k+2} piece j - 4: A_{k+1} needs 9 (4) newer in flight, B_{k+1} 7 (0)
+#if NERF_WGRAD_SPLITPOS == 1   // (study) later: A at tiles 5, 6, B both at 7
+        if constexpr (j == 5) vm_wait_n(nxt2 ? 10 : 4);
+        if constexpr (j == 7) vm_wait_n(nxt2 ? 8 : 0);
+        if constexpr (j == 5 || j == 6) split_own(2 * k + 2, j - 5, sa, true);
+        if constexpr (j == 7) { split_own(2 * k + 3, 0, sb, false); split_own(2 * k + 3, 1, sb, false); }
+#elif NERF_WGRAD_SPLITPOS == 2   // (study) earlier: A at tiles 2, 3, B at 4, 5
+        if constexpr (j == 2) vm_wait_n(nxt2 ? 7 : 4);
+        if constexpr (j == 4) vm_wait_n(nxt2 ? 5 : 0);
+        if constexpr (j == 2 || j == 3) split_own(2 * k + 2, j - 2, sa, true);
+        if constexpr (j == 4 || j == 5) split_own(2 * k + 3, j - 4, sb, false);
+#else
         if constexpr (j == 4) vm_wait_n(nxt2 ? 9 : 4);
         if constexpr (j == 6) vm_wait_n(nxt2 ? 7 : 0);
         if constexpr (j == 4 || j == 5) split_own(2 * k + 2, j - 4, sa, true);
         if constexpr (j == 6 || j == 7) split_own(2 * k + 3, j - 6, sb, false);
+#endif
       }
     };
     tile(std::integral_constant<int, 0>{});

@@ -8,6 +8,9 @@ between such a read and its drain that reads or writes one of the pending
 destination VGPRs or AGPRs (a stale read, or a register the late data would
 clobber).
 
+A counted wait lgkmcnt(N) retires the reads with at least N LGKM operations
+issued after them (LDS returns in order), unless an SMEM / FLAT operation
+(out of order) is outstanding: then only lgkmcnt(0) drains.
 The pending set is propagated over the control-flow graph of the .s (basic
 blocks split at labels and branches; successors from s_branch / s_cbranch_* /
 fall-through), so reads left in flight across a loop back edge or a branch
@@ -86,34 +89,61 @@ def _blocks(ins, labels):
     return bounds, succ
 
 
+LGKM_CNT = re.compile(r"lgkmcnt\((\d+)\)")
+SMEM = "__smem__"   # an SMEM / FLAT op since the last full drain: counted waits prove nothing
+
+
+def _lgkm_op(op):
+    """Does the instruction count in lgkmcnt? ('lds' in order, 'smem' not)."""
+    if op.startswith("ds_") and op not in ("ds_nop",):
+        return "lds"
+    if op.startswith("s_load") or op.startswith("s_buffer_load") or op.startswith("flat_") \
+            or op.startswith("s_memtime") or op.startswith("s_memrealtime"):
+        return "smem"
+    return None
+
+
 def _run_block(ins, s, e, pending, report):
+    # pending: register -> (line of the asm read that targets it, number of
+    # LGKM ops issued after that read). LDS ops return in order, so a counted
+    # wait lgkmcnt(N) retires every read with at least N LGKM ops behind it --
+    # unless an SMEM / FLAT op (which may return out of order) is outstanding.
     pending = dict(pending)
     for p in range(s, e):
         line, t, in_asm = ins[p]
         if t is None:
             continue
         op = t.split()[0]
-        if op == "s_waitcnt" and "lgkmcnt(0)" in t:
-            pending.clear()
+        if op == "s_waitcnt" and "lgkmcnt" in t:
+            n = int(LGKM_CNT.search(t).group(1))
+            if n == 0:
+                pending.clear()
+            elif SMEM not in pending:
+                pending = {r: v for r, v in pending.items() if v[1] < n}
             continue
+        kind = _lgkm_op(op)
         ops = [x.strip() for x in t[len(op):].split(",")]
         used = set()
         for o in ops:
             used |= regs(o.split()[0] if o else "")
+        if kind:
+            pending = {r: (v if r == SMEM else (v[0], v[1] + 1)) for r, v in pending.items()}
+            if kind == "smem" and pending:
+                pending[SMEM] = (line + 1, 0)
         if in_asm and op.startswith("ds_read"):
             # another asm read into a pending register is harmless (LDS returns in
             # order: the later read's data land last), e.g. a fragment group the
             # compiler found dead re-using one destination; any other access is not
             dst = regs(ops[0])
             for r in dst:
-                pending[r] = line + 1
+                pending[r] = (line + 1, 0)
             continue
         if op.startswith("s_") and not op.startswith("s_waitcnt"):
             continue
         hit = used & set(pending)
         if hit:
             report(line, f"'{t}' touches pending LDS-read regs {sorted(hit)} "
-                         f"(read issued at line {pending[min(hit)]})")
+                         f"(read issued at line {pending[min(hit)][0]})")
     return pending
 
 
@@ -138,6 +168,9 @@ def main(path):
             changed = not seen[n]
             for r, v in out.items():
                 if r not in merged:
+                    merged[r] = v
+                    changed = True
+                elif r != SMEM and v[1] < merged[r][1]:   # the most recent on any path
                     merged[r] = v
                     changed = True
             if changed:
