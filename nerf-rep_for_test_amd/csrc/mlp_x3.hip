@@ -425,6 +425,9 @@ struct ActStore {
   unsigned wb;                 // bits of the current 4-tile block
   bool bits, valid;
   bool on = true;              // uniform: false = these rows are not stored (null output)
+  __device__ __forceinline__ void st32(float x, unsigned vo, int off) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (int)vo, off, NERF_ACT_STORE_AUX);
+  }
   template <bool T>
   __device__ __forceinline__ void set_lay(const Lay& L, int64_t tile, int wave) {
     if constexpr (T) {
@@ -447,10 +450,8 @@ struct ActStore {
   __device__ __forceinline__ void part(const Op& v) {
     if (!on) return;
     const unsigned vo = lane_off();
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[R]), rs, (int)vo,
-                                          (int)(2 * G * ts + R * rstr), NERF_ACT_STORE_AUX);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + R]), rs, (int)vo,
-                                          (int)((2 * G + 1) * ts + R * rstr), NERF_ACT_STORE_AUX);
+    st32(v[R], vo, (int)(2 * G * ts + R * rstr));
+    st32(v[4 + R], vo, (int)((2 * G + 1) * ts + R * rstr));
     if constexpr (R == 3) store_bits<G>(v);
   }
   template <int G>
@@ -475,18 +476,18 @@ struct ActStore {
   template <int G>
   __device__ __forceinline__ void pair(const Op& v) {
     if (!on) return;
-#if NERF_ABL_NOSTORE   // timing-only ablation build: no row / bit stores (wrong results)
+#if NERF_ABL_NOSTORE == 1   // timing-only ablation build: no row / bit stores (wrong results)
     asm volatile("" ::"v"(v));
     return;
+#elif NERF_ABL_NOSTORE == 2   // timing-only: the stores issued, all dropped by the range check
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)nullptr, 0, 0, 0x00020000);
+    rb = rs;
 #endif
     const unsigned vo = lane_off();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rs, (int)vo,
-                                            (int)(2 * G * ts + r * rstr), NERF_ACT_STORE_AUX);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[4 + r]), rs, (int)vo,
-                                            (int)((2 * G + 1) * ts + r * rstr),
-                                            NERF_ACT_STORE_AUX);
+      st32(v[r], vo, (int)(2 * G * ts + r * rstr));
+      st32(v[4 + r], vo, (int)((2 * G + 1) * ts + r * rstr));
     }
     store_bits<G>(v);
   }
