@@ -1912,7 +1912,9 @@ __device__ __forceinline__ void wgrad_dma_body(
   for (int k = 0; k < nsteps; ++k) {
     // step k's fragments were split by their owners (the prologue or step k - 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if NERF_WGRAD_ABL != 4   // 4: timing-only ablation without the step barrier (races)
     __builtin_amdgcn_s_barrier();   // every split visible; B_{k-1}'s slot is free
+#endif
     asm volatile("" ::: "memory");
     // A_{k+2} into B_{k-1}'s slot from the start of the step; B_{k+2} into A_k's
     // slot after the mid-step barrier (every wave holds its A_k fragments). This
@@ -1967,7 +1969,9 @@ __device__ __forceinline__ void wgrad_dma_body(
 #endif
       const half8 bh = __builtin_bit_cast(half8, cur.x), bl = __builtin_bit_cast(half8, cur.y);
       if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
+#if NERF_WGRAD_ABL != 3   // 3: timing-only ablation without the mid-step barrier (races)
       if constexpr (j == 4) __builtin_amdgcn_s_barrier();
+#endif
       if constexpr (j < 4) issue_piece(ga, std::integral_constant<int, j>{});
       else issue_piece(gb, std::integral_constant<int, j - 4>{});
 #pragma unroll
