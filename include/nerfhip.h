@@ -41,7 +41,7 @@ const char* nerf_last_error(void);
  * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4; 3: NerfWgradDesc
  * bsa / bsb, NerfX3TrainOut.bs / NerfX3BwdIO.bs and the encoding-backward layout
  * arguments: the T16 activation layout of round 5) */
-#define NERF_ABI_VERSION 3
+#define NERF_ABI_VERSION 4
 int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
  * source tree this library was compiled from (nerfhip/_lib.py refuses a
@@ -255,6 +255,10 @@ typedef struct NerfWgradDesc {
                              feature-major rows ([M][ld], ld >= P); 16 * rows with ld = 16:
                              the 16-sample block layout [P / 16][rows][16] of the fused
                              training kernels (nerf_mlp_train_forward_x3) */
+  int a2_row;             /* (ABI 4) 0: amax_a2 widens the one A scale, as above. > 0 (a
+                             multiple of 16, < M, amax_a2 set): rows < a2_row of A take
+                             the scale of *amax_a, rows >= a2_row that of *amax_a2 -- two
+                             row blocks of one operand with their own FP16 split ranges */
 } NerfWgradDesc;
 int nerf_x3_wgrad_batch(const NerfWgradDesc* descs, int n, int chunks, nerf_stream_t stream);
 /* The same with a K split per output tile: tile_chunks[t] (1 .. zmax, < 256)

@@ -1761,44 +1761,42 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_kernel(
 
 // The same partial weight gradients for aligned operands (host-checked: P a
 // multiple of 32, 16-B rows, operands < 2 GiB): the raw FP32 K steps land in
-// LDS by buffer-form LDS-DMA, so no registers hold in-flight data; each wave
-// splits the fragments it reads (FP32 -> FP16 hi/lo) in registers. A K step
+// LDS by buffer-form LDS-DMA, so no registers hold in-flight data. A K step
 // (32 samples) is two granules of 32 KiB, A_k (256 rows of A) then B_k, and
 // the granules stream through a 5-slot ring (160 KiB, all of the CU's LDS):
-// while step k is multiplied, A_{k+1}, B_{k+1}, A_{k+2} and B_{k+2} are
-// landing -- B_{k+2} in A_k's slot, freed by a mid-step barrier once every wave
-// holds its A_k fragments (before it, a B granule was issued one step ahead
-// and had about one step to land). A wave's 8 LDS-DMA pieces of a step (4 of
+// while step k is multiplied, A_{k+1} and B_{k+1} are split and A_{k+2},
+// B_{k+2} are landing -- B_{k+2} in A_k's slot, freed by a mid-step barrier once
+// every wave holds its A_k fragments. A wave's 8 LDS-DMA pieces of a step (4 of
 // A_{k+2}, then 4 of B_{k+2}) are issued one per B tile of its MFMA loop, so
-// their issue cost overlaps the MFMAs (issued all at once after the step's
-// barrier, every wave of the CU stalled on them together with the MFMA pipes
-// idle).
+// their issue cost overlaps the MFMAs.
 // Piece (t, h) of a granule = 16-row tile t, half h: lane l holds row
 // 16t + (l & 15), samples 8 (l >> 4) + 4h .. +3, so the two halves read by
 // lane l are one MFMA fragment (row l & 15, samples 8 (l >> 4) .. +7). Rows past
-// M / N read 0 (offset past num_records). Bias sums from the A fragments
-// (waves nb = 0). The body for output tile (mtile, ntile) and K subset z of Z;
-// subset z's partials go to part + z * ldpart ([M][N]) and bias_part + z *
-// ldbias ([M]).
+// M / N read 0 (offset past num_records).
+// Self split (round 5): a wave splits, in place, the fragments of the pieces it
+// issued itself (granule g, tiles 2 wave + t, both halves: FP32 -> FP16 hi in
+// half 0, lo in half 1), once its own vmcnt says they landed -- no barrier
+// between the landing and the split; the MFMA loop reads (hi, lo) as they are.
+// Every element is split once instead of by every wave that multiplies it (A
+// twice, B four times): 64 instead of 192 VALU per wave and step, partials bit
+// for bit those of the per-wave split. A granules add their raw values to rs
+// (the bias sums: tile 2 wave + t, this lane's row and 8 samples).
+// Scales: per tensor (amax_a, amax_b), or two for A (a2_row > 0: rows >=
+// a2_row, whole 16-row tiles, split at amax_a2's scale and undone with it).
+// The body for output tile (mtile, ntile) and K subset z of Z; subset z's
+// partials go to part + z * ldpart ([M][ldo]) and bias_part + z * ldbias ([M]).
+// NERF_WGRAD_ABL (timing-only study builds, results invalid): 1 no MFMAs, 2 no
+// operand stream, 3 no mid-step barrier, 4 no step barrier.
 constexpr int kWgRing = 5;
 #ifndef NERF_WGRAD_ABL
 #define NERF_WGRAD_ABL 0
 #endif
-#ifndef NERF_WGRAD_EARLY   // (study builds) counted drains of the step's first reads
-#define NERF_WGRAD_EARLY 0
-#endif
-#ifndef NERF_WGRAD_SPLITPOS   // (study builds) where the next step's split runs
-#define NERF_WGRAD_SPLITPOS 0
-#endif
-#ifndef NERF_WGRAD_SELFSPLIT   // 0: every wave splits the fragments it reads (round 4)
-#define NERF_WGRAD_SELFSPLIT 1
-#endif
 __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
-    const float amax_b, float* __restrict__ part, int64_t ldpart,
-    float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z, int Z,
-    int64_t ldo, int64_t bsa, int64_t bsb) {
+    const float amax_a2, int a2_row, const float amax_b, float* __restrict__ part,
+    int64_t ldpart, float* __restrict__ bias_part, int64_t ldbias, int mtile, int ntile, int z,
+    int Z, int64_t ldo, int64_t bsa, int64_t bsb) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: SGPR rsrc / M0
@@ -1806,8 +1804,11 @@ __device__ __forceinline__ void wgrad_dma_body(
   const int64_t pb = (int64_t)z * 32, kstride = (int64_t)Z * 32;
   const int nsteps = pb < P ? (int)((P - pb + kstride - 1) / kstride) : 0;
   const int ngran = 2 * nsteps;
-  const int ea = act_exponent(amax_a), eb = act_exponent(amax_b);
-  const float sa = ldexpf(1.0f, ea), sb = ldexpf(1.0f, eb);
+  const int ea = act_exponent(amax_a), ea2 = act_exponent(amax_a2), eb = act_exponent(amax_b);
+  const float sb = ldexpf(1.0f, eb);
+  // this wave's two A tiles (rows m0 + 16 (2 wave + t)): their scale
+  const float sa0 = ldexpf(1.0f, m0 + 32 * wave >= a2_row ? ea2 : ea);
+  const float sa1 = ldexpf(1.0f, m0 + 32 * wave + 16 >= a2_row ? ea2 : ea);
 
   // this wave's 4 pieces of every granule: q = 4 wave + i (tile q >> 1, half q & 1).
   // Element (r, p) of an operand: r * ld + (p >> 4) * bs + (p & 15) (bs 16:
@@ -1838,7 +1839,7 @@ __device__ __forceinline__ void wgrad_dma_body(
   auto issue_piece = [&](int g, auto Ic) {
     constexpr int I = decltype(Ic)::value;
     if (g >= ngran) return;
-#if NERF_WGRAD_ABL == 2   // timing-only ablation: no operand stream (stale LDS)
+#if NERF_WGRAD_ABL == 2
     return;
 #endif
     const int64_t p0 = pb + (int64_t)(g >> 1) * kstride;   // a multiple of 32
@@ -1866,25 +1867,14 @@ __device__ __forceinline__ void wgrad_dma_body(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4(0.0f);
 
-  // the raw FP32 fragment of a tile: its two pieces (halves), 1 KiB apart
-  // Raw: the two halves as the asm wrote them. A drain names every pending Raw
-  // as an in/out operand, so no copy or shuffle of one can run before it lands.
+  // a fragment's two halves (hi, lo) as the asm wrote them, 1 KiB apart. A drain
+  // names every pending Raw as an in/out operand, so no copy of one can run
+  // before it lands.
   struct Raw { u32x4 x, y; };
   auto read_pair = [&](unsigned addr, Raw& r) {   // addr: LDS byte address of half 0
     asm volatile("ds_read_b128 %0, %1" : "=v"(r.x) : "v"(addr) : "memory");
     asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(r.y) : "v"(addr) : "memory");
   };
-
-#if NERF_WGRAD_SELFSPLIT
-  // Self split: a wave splits, in place, the fragments of the pieces it issued
-  // itself (granule g, tiles 2 wave + t, both halves), once its own vmcnt says
-  // they landed -- no barrier between the landing and the split. Half 0 then
-  // holds the FP16 hi pairs, half 1 the lo pairs, so the MFMA loop's read_pair
-  // yields (hi, lo) with no split of its own: every element is split once, not
-  // once per wave that multiplies it (A twice, B four times). Operands and
-  // their MFMA order are unchanged (bit-identical partials). A granules add
-  // their raw values to rs (the bias sums: tile 2 wave + t, this lane's row and
-  // 8 samples, in the same order as the fragment reads did).
   float rs[2] = {0.0f, 0.0f};
   auto split_own = [&](int g, int t, float s, bool sum) {
     u32x4* q = reinterpret_cast<u32x4*>(&ring[g % kWgRing][(2 * (2 * wave + t)) * 64 + lane]);
@@ -1898,28 +1888,30 @@ __device__ __forceinline__ void wgrad_dma_body(
     q[0] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 0, 1, 2, 3));
     q[64] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 4, 5, 6, 7));
   };
+  auto split_a = [&](int g, int t) { split_own(g, t, t ? sa1 : sa0, true); };
+  auto split_b = [&](int g, int t) { split_own(g, t, sb, false); };
 
   // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1), then this wave's share of step 0
   for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
   if (nsteps > 0) {
     vm_wait_n(nsteps > 1 ? 12 : 4);   // A_0 landed
-    split_own(0, 0, sa, true);
-    split_own(0, 1, sa, true);
+    split_a(0, 0);
+    split_a(0, 1);
     vm_wait_n(nsteps > 1 ? 8 : 0);    // B_0 landed
-    split_own(1, 0, sb, false);
-    split_own(1, 1, sb, false);
+    split_b(1, 0);
+    split_b(1, 1);
   }
   for (int k = 0; k < nsteps; ++k) {
     // step k's fragments were split by their owners (the prologue or step k - 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if NERF_WGRAD_ABL != 4   // 4: timing-only ablation without the step barrier (races)
+#if NERF_WGRAD_ABL != 4
     __builtin_amdgcn_s_barrier();   // every split visible; B_{k-1}'s slot is free
 #endif
     asm volatile("" ::: "memory");
     // A_{k+2} into B_{k-1}'s slot from the start of the step; B_{k+2} into A_k's
-    // slot after the mid-step barrier (every wave holds its A_k fragments). This
-    // wave splits its share of A_{k+1} at B tiles 4-5 and of B_{k+1} at 6-7: A
-    // lands in 1.5 steps, B in about 1.25.
+    // slot after the mid-step barrier. This wave splits its share of A_{k+1} at
+    // B tiles 4-5 and of B_{k+1} at 6-7: A lands in 1.5 steps, B in about 1.25
+    // (later or earlier splits: within 1.5 %, profiles/r5_wgrad_selfsplit/)
     const int ga = 2 * k + 4, gb = 2 * k + 5;
     const bool nxt = k + 1 < nsteps, nxt2 = k + 2 < nsteps;
     if (!busy) {   // nothing to multiply: stage and split this wave's pieces
@@ -1927,28 +1919,20 @@ __device__ __forceinline__ void wgrad_dma_body(
       __builtin_amdgcn_s_barrier();
       if (nxt) {
         vm_wait_n(nxt2 ? 8 : 4);
-        split_own(2 * k + 2, 0, sa, true);
-        split_own(2 * k + 2, 1, sa, true);
+        split_a(2 * k + 2, 0);
+        split_a(2 * k + 2, 1);
       }
       issue(gb);
       if (nxt) {
         vm_wait_n(nxt2 ? 8 : 0);
-        split_own(2 * k + 3, 0, sb, false);
-        split_own(2 * k + 3, 1, sb, false);
+        split_b(2 * k + 3, 0);
+        split_b(2 * k + 3, 1);
       }
       continue;
     }
     const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
     const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
     Raw ra[4], rb[2];
-#if NERF_WGRAD_EARLY
-    // A fragment 0 and B tile 0 first: tile 0's products of A fragment i start
-    // as soon as its reads are in (counted drains below), not after all ten
-    read_pair(baseA + (unsigned)((4 * mb) * 2048), ra[0]);
-    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);   // B tile nt = 8 nb + j
-#pragma unroll
-    for (int i = 1; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
-#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
     read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);   // B tile nt = 8 nb + j
@@ -1958,66 +1942,33 @@ __device__ __forceinline__ void wgrad_dma_body(
                    "+v"(rb[0].x), "+v"(rb[0].y)
                  :
                  : "memory");
-#endif
     auto tile = [&](auto Jc) {
       constexpr int j = decltype(Jc)::value;
       Raw& cur = rb[j & 1];
       if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
-#if NERF_WGRAD_EARLY   // A fragment 0 and B tile 0 in; A fragments 1-3 (6 reads) may be in flight
-      if constexpr (j == 0)
-        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(cur.x), "+v"(cur.y) : : "memory");
-#endif
       const half8 bh = __builtin_bit_cast(half8, cur.x), bl = __builtin_bit_cast(half8, cur.y);
       if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
-#if NERF_WGRAD_ABL != 3   // 3: timing-only ablation without the mid-step barrier (races)
+#if NERF_WGRAD_ABL != 3
       if constexpr (j == 4) __builtin_amdgcn_s_barrier();
 #endif
       if constexpr (j < 4) issue_piece(ga, std::integral_constant<int, j>{});
       else issue_piece(gb, std::integral_constant<int, j - 4>{});
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-#if NERF_WGRAD_EARLY
-        if constexpr (j == 0) {   // in flight behind A fragment i: the later ones and B tile 1
-          if (i == 0)
-            ;
-          else if (i == 1)
-            asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(ra[1].x), "+v"(ra[1].y) : : "memory");
-          else if (i == 2)
-            asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(ra[2].x), "+v"(ra[2].y) : : "memory");
-          else
-            asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(ra[3].x), "+v"(ra[3].y) : : "memory");
-          __builtin_amdgcn_sched_barrier(0);   // keep each drain right before its products
-        }
-#endif
         const half8 ah = __builtin_bit_cast(half8, ra[i].x), al = __builtin_bit_cast(half8, ra[i].y);
-#if NERF_WGRAD_ABL == 1   // timing-only ablation: no MFMAs (operands kept live)
+#if NERF_WGRAD_ABL == 1
         asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
 #else
         acc[i][j] = MFMA16(ah, bh, acc[i][j]);
         acc[i][j] = MFMA16(ah, bl, acc[i][j]);
         acc[i][j] = MFMA16(al, bh, acc[i][j]);
 #endif
-#if NERF_WGRAD_EARLY
-        if constexpr (j == 0) __builtin_amdgcn_sched_barrier(0);
-#endif
       }
       if (nxt) {   // after B_{k+2} piece j - 4: A_{k+1} needs 9 (4) newer in flight, B_{k+1} 7 (0)
-#if NERF_WGRAD_SPLITPOS == 1   // (study) later: A at tiles 5, 6, B both at 7
-        if constexpr (j == 5) vm_wait_n(nxt2 ? 10 : 4);
-        if constexpr (j == 7) vm_wait_n(nxt2 ? 8 : 0);
-        if constexpr (j == 5 || j == 6) split_own(2 * k + 2, j - 5, sa, true);
-        if constexpr (j == 7) { split_own(2 * k + 3, 0, sb, false); split_own(2 * k + 3, 1, sb, false); }
-#elif NERF_WGRAD_SPLITPOS == 2   // (study) earlier: A at tiles 2, 3, B at 4, 5
-        if constexpr (j == 2) vm_wait_n(nxt2 ? 7 : 4);
-        if constexpr (j == 4) vm_wait_n(nxt2 ? 5 : 0);
-        if constexpr (j == 2 || j == 3) split_own(2 * k + 2, j - 2, sa, true);
-        if constexpr (j == 4 || j == 5) split_own(2 * k + 3, j - 4, sb, false);
-#else
         if constexpr (j == 4) vm_wait_n(nxt2 ? 9 : 4);
         if constexpr (j == 6) vm_wait_n(nxt2 ? 7 : 0);
-        if constexpr (j == 4 || j == 5) split_own(2 * k + 2, j - 4, sa, true);
-        if constexpr (j == 6 || j == 7) split_own(2 * k + 3, j - 6, sb, false);
-#endif
+        if constexpr (j == 4 || j == 5) split_a(2 * k + 2, j - 4);
+        if constexpr (j == 6 || j == 7) split_b(2 * k + 3, j - 6);
       }
     };
     tile(std::integral_constant<int, 0>{});
@@ -2039,115 +1990,22 @@ __device__ __forceinline__ void wgrad_dma_body(
       if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
     }
   }
-#else
-  float rs4[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's share of sum_p A (nb = 0)
-  auto to_op = [](const Raw& r) {
-    return __builtin_bit_cast(Op, __builtin_shufflevector(r.x, r.y, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1)
-  for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
-  for (int k = 0; k < nsteps; ++k) {
-    // granules <= 2k+1 landed (this wave's pieces); 2k+2, 2k+3 (8 pieces) may stay in flight
-    if (k + 1 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // everyone's landed; B_{k-1}'s slot is free
-    asm volatile("" ::: "memory");
-    // A_{k+2} into B_{k-1}'s slot from the start of the step; B_{k+2} into A_k's
-    // slot after a mid-step barrier (every wave holds its A_k fragments by then),
-    // so a B granule has 1.5 steps to land instead of one
-    const int ga = 2 * k + 4, gb = 2 * k + 5;
-    if (!busy) {   // nothing to multiply: stage this wave's pieces at once
-      issue(ga);
-      __builtin_amdgcn_s_barrier();
-      issue(gb);
-      continue;
-    }
-    const unsigned baseA = lds_addr((const float*)&ring[(2 * k) % kWgRing][0]) + lane * 16u;
-    const unsigned baseB = lds_addr((const float*)&ring[(2 * k + 1) % kWgRing][0]) + lane * 16u;
-    // The A fragments and the first B fragment are read together; the A split
-    // runs tile by tile inside the first B tile's MFMAs (each A tile split just
-    // before its own three products), so it is not a VALU-only phase at the
-    // start of every step.
-    half8 ah[4], al[4];
-    Raw ra[4], rb[2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) read_pair(baseA + (unsigned)((4 * mb + i) * 2048), ra[i]);
-    // B tile nt = 8 nb + j
-    read_pair(baseB + (unsigned)((8 * nb) * 2048), rb[0]);
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(ra[0].x), "+v"(ra[0].y), "+v"(ra[1].x), "+v"(ra[1].y),
-                   "+v"(ra[2].x), "+v"(ra[2].y), "+v"(ra[3].x), "+v"(ra[3].y),
-                   "+v"(rb[0].x), "+v"(rb[0].y)
-                 :
-                 : "memory");
-    auto tile = [&](auto Jc) {
-      constexpr int j = decltype(Jc)::value;
-      Raw& cur = rb[j & 1];
-      if constexpr (j > 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur.x), "+v"(cur.y) : : "memory");
-      Op b = to_op(cur);
-      if constexpr (j + 1 < 8) read_pair(baseB + (unsigned)((8 * nb + j + 1) * 2048), rb[(j + 1) & 1]);
-      // one LDS-DMA piece per B tile: A_{k+2} pieces 0-3, the mid-step barrier,
-      // then B_{k+2} pieces 0-3
-      if constexpr (j == 4) __builtin_amdgcn_s_barrier();
-      if constexpr (j < 4) issue_piece(ga, std::integral_constant<int, j>{});
-      else issue_piece(gb, std::integral_constant<int, j - 4>{});
-      split_op(b, sb);
-      const half8 bh = op_hi(b), bl = op_lo(b);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (j == 0) {
-          Op v = to_op(ra[i]);
-          if (nb == 0) {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) rs4[i] += v[t];
-          }
-          split_op(v, sa);
-          ah[i] = op_hi(v);
-          al[i] = op_lo(v);
-        }
-#if NERF_WGRAD_ABL == 1   // timing-only ablation: no MFMAs (operands kept live)
-        asm volatile("" ::"v"(ah[i]), "v"(al[i]), "v"(bh), "v"(bl));
-#else
-        acc[i][j] = MFMA16(ah[i], bh, acc[i][j]);
-        acc[i][j] = MFMA16(ah[i], bl, acc[i][j]);
-        acc[i][j] = MFMA16(al[i], bh, acc[i][j]);
-#endif
-      }
-    };
-    tile(std::integral_constant<int, 0>{});
-    tile(std::integral_constant<int, 1>{});
-    tile(std::integral_constant<int, 2>{});
-    tile(std::integral_constant<int, 3>{});
-    tile(std::integral_constant<int, 4>{});
-    tile(std::integral_constant<int, 5>{});
-    tile(std::integral_constant<int, 6>{});
-    tile(std::integral_constant<int, 7>{});
-  }
-  if (bias_part && ntile == 0 && nb == 0 && busy) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {   // row 16 (4 mb + i) + (l & 15): lanes l, l^16, l^32, l^48
-      float r = rs4[i];
-      r += __shfl_xor(r, 16);
-      r += __shfl_xor(r, 32);
-      const int row = m0 + 16 * (4 * mb + i) + lane;
-      if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
-    }
-  }
-#endif
   if (!busy) return;
-  const float inv = ldexpf(1.0f, -(ea + eb));
   float* out = part + (int64_t)z * ldpart;
   const int g4 = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int mt = m0 + 64 * mb + 16 * i;   // this A tile's first row: its scale
+    const float inv = ldexpf(1.0f, -((mt >= a2_row ? ea2 : ea) + eb));
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 64 * mb + 16 * i + 4 * g4 + r;
+        const int m = mt + 4 * g4 + r;
         const int n = n0 + 128 * nb + 16 * j + (lane & 15);
         if (m < M && n < N) out[(int64_t)m * ldo + n] = acc[i][j][r] * inv;
       }
+  }
 }
 
 __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
@@ -2155,8 +2013,9 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_dma_kernel(
     int N, int64_t P, const float* __restrict__ amax_a, const float* __restrict__ amax_b,
     float* __restrict__ part, float* __restrict__ bias_part) {
   __shared__ __attribute__((aligned(16))) uint4 ring[kWgRing][32 * 64];
-  wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, *amax_a, *amax_b, part, (int64_t)M * N, bias_part,
-                 M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, N, 16, 16);
+  wgrad_dma_body(ring, A, lda, M, B, ldb, N, P, *amax_a, *amax_a, 1 << 30, *amax_b, part,
+                 (int64_t)M * N, bias_part, M, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, N,
+                 16, 16);
 }
 
 // Several weight gradients in one launch (the whole backward of a network):
@@ -2185,13 +2044,16 @@ __global__ __launch_bounds__(kTrainThreads, 2) void x3_wgrad_batch_kernel(const 
   const int z = w - (bt.t_wg_end[t] - Z);
   const NerfWgradDesc& d = bt.d[bt.t_desc[t]];
   const int mtile = bt.t_m[t], ntile = bt.t_n[t];
-  // a scale may cover two tensors' maxima (rows of two producers in one operand)
-  const float ma = d.amax_a2 ? fmaxf(*d.amax_a, *d.amax_a2) : *d.amax_a;
+  // a scale may cover two tensors' maxima (rows of two producers in one operand),
+  // or A's two row blocks take one each (a2_row)
+  const bool two = d.amax_a2 && d.a2_row > 0;
+  const float ma = d.amax_a2 && !two ? fmaxf(*d.amax_a, *d.amax_a2) : *d.amax_a;
+  const float ma2 = two ? *d.amax_a2 : ma;
   const float mb = d.amax_b2 ? fmaxf(*d.amax_b, *d.amax_b2) : *d.amax_b;
   const int64_t ldo = d.ldo ? d.ldo : d.N;
-  wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, ma, mb, d.part,
-                 d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z, ldo, d.bsa ? d.bsa : 16,
-                 d.bsb ? d.bsb : 16);
+  wgrad_dma_body(ring, d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, ma, ma2, two ? d.a2_row : 1 << 30,
+                 mb, d.part, d.ldpart, d.bias_part, d.ldbias, mtile, ntile, z, Z, ldo,
+                 d.bsa ? d.bsa : 16, d.bsb ? d.bsb : 16);
   if (z != 0 || Z >= bt.Zmax) return;
   // zeros in the partial rows Z .. Zmax-1 of this tile (and of its bias rows)
   const int m0 = mtile * kWgTile, n0 = ntile * kWgTile;
@@ -2627,7 +2489,9 @@ extern "C" int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const in
                      d.P >= 0 && (bsa == 16 ? d.lda >= d.P : bsa % 256 == 0 && bsa >= 16 * d.M) &&
                      (bsb == 16 ? d.ldb >= d.P : bsb % 256 == 0 && bsb >= 16 * d.N) && ldo >= d.N &&
                      d.ldpart >= (int64_t)(d.M - 1) * ldo + d.N &&
-                     (!d.bias_part || d.ldbias >= d.M),
+                     (!d.bias_part || d.ldbias >= d.M) &&
+                     (d.a2_row == 0 || (d.amax_a2 && d.a2_row > 0 && d.a2_row % 16 == 0 &&
+                                        d.a2_row < d.M)),
                  "nerf_x3_wgrad_batch: bad descriptor");
     NERF_REQUIRE(wgrad_dma_ok(d.A, d.lda, d.M, d.B, d.ldb, d.N, d.P, bsa, bsb),
                  "nerf_x3_wgrad_batch: operands must be aligned (P % 32 == 0, 16-B rows, < 2 GiB)");

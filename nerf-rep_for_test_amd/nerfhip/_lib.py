@@ -10,7 +10,7 @@ import os
 import threading
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ABI_VERSION = 3   # include/nerfhip.h NERF_ABI_VERSION
+ABI_VERSION = 4   # include/nerfhip.h NERF_ABI_VERSION
 LIB_PATH = os.environ.get("NERFHIP_LIB", os.path.join(PKG_ROOT, "lib", "libnerfhip.so"))
 
 MLP_SLICES = 73

@@ -528,7 +528,8 @@ class _WgradDesc(ctypes.Structure):
                 ("ldpart", ctypes.c_int64), ("bias_part", ctypes.c_void_p),
                 ("ldbias", ctypes.c_int64), ("M", ctypes.c_int), ("N", ctypes.c_int),
                 ("amax_a2", ctypes.c_void_p), ("amax_b2", ctypes.c_void_p),
-                ("ldo", ctypes.c_int64), ("bsa", ctypes.c_int64), ("bsb", ctypes.c_int64)]
+                ("ldo", ctypes.c_int64), ("bsa", ctypes.c_int64), ("bsb", ctypes.c_int64),
+                ("a2_row", ctypes.c_int)]
 
 
 _NCU = {}
@@ -668,16 +669,22 @@ class WgradBatch:
         self.device = device
         self.req = []
 
-    def add(self, A, B, amax_a=None, amax_b=None, with_bias=False, width=None, into=None):
+    def add(self, A, B, amax_a=None, amax_b=None, with_bias=False, width=None, into=None,
+            a_split=0):
         """width: the result has `width` columns, B's rows the first of them;
         into = (slot, c0): B's rows are columns c0 .. of slot's result (the
         same A; no result of its own). One contiguous gradient from operands in
-        two buffers (the skip layer's [encoding | h4])."""
+        two buffers (the skip layer's [encoding | h4]).
+        amax_a = (m1, m2) with a_split = r (a multiple of 16): A's rows < r take
+        m1's FP16 split range, rows >= r m2's (two producers' rows in one
+        operand, each at its own scale); a_split 0: one scale, max(m1, m2)."""
         if amax_a is None:
             amax_a = _absmax(A.dense() if isinstance(A, BlockRows) else A)
         if amax_b is None:
             amax_b = _absmax(B.dense() if isinstance(B, BlockRows) else B)
-        self.req.append((A, B, amax_a, amax_b, with_bias, width, into))
+        assert not a_split or (isinstance(amax_a, tuple) and a_split % 16 == 0
+                               and 0 < a_split < A.shape[0])
+        self.req.append((A, B, amax_a, amax_b, with_bias, width, into, a_split))
         return len(self.req) - 1
 
     def results(self):
@@ -694,8 +701,18 @@ class WgradBatch:
             one = lambda m: torch.maximum(*m) if isinstance(m, tuple) else m   # noqa: E731
             dn = lambda t: t.dense() if isinstance(t, BlockRows) else t   # noqa: E731
             assert not blocked or P % 32 != 0, "block-layout operands the batch cannot take"
-            res = [_wgrad(dn(A), dn(B), one(aa), one(ab), wb) for A, B, aa, ab, wb, _, _ in req]
-            for k, (A, B, _, _, wb, width, into) in enumerate(req):
+
+            def wg(A, B, aa, ab, wb, r):
+                if not r:
+                    return _wgrad(dn(A), dn(B), one(aa), one(ab), wb)
+                # two row blocks of A, each at its own scale (as the batched kernel)
+                lo, hi = (_wgrad(dn(A)[rows], dn(B), m, one(ab), wb)
+                          for rows, m in ((slice(0, r), aa[0]), (slice(r, None), aa[1])))
+                if wb:
+                    return torch.cat([lo[0], hi[0]]), torch.cat([lo[1], hi[1]])
+                return torch.cat([lo, hi])
+            res = [wg(A, B, aa, ab, wb, r) for A, B, aa, ab, wb, _, _, r in req]
+            for k, (A, B, _, _, wb, width, into, _) in enumerate(req):
                 if into is not None:   # the column blocks joined on the host
                     s, c0 = into
                     tgt = res[s][0] if isinstance(res[s], tuple) else res[s]
@@ -713,11 +730,11 @@ class WgradBatch:
         # output regions: [M][width] per request that owns one; joined requests
         # write their column block of the owner's region
         region, ld = {}, 0
-        for k, (A, B, _, _, _, width, into) in enumerate(req):
+        for k, (A, B, _, _, _, width, into, _) in enumerate(req):
             if into is None:
                 region[k] = (ld, width or B.shape[0])
                 ld += A.shape[0] * (width or B.shape[0])
-        bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb, _, _ in req]
+        bsizes = [A.shape[0] if wb else 0 for A, _, _, _, wb, _, _, _ in req]
         ldb = sum(bsizes)
         # weight and bias partials side by side in one [Z][ld + ldb] array: one
         # fixed-order sum for both
@@ -727,7 +744,7 @@ class WgradBatch:
         boff = 0
         def two(m):   # a scale given as (tensor, tensor): the kernel takes their max
             return (m[0].data_ptr(), m[1].data_ptr()) if isinstance(m, tuple) else (m.data_ptr(), None)
-        for k, (A, B, aa, ab, wb, width, into) in enumerate(req):
+        for k, (A, B, aa, ab, wb, width, into, a_split) in enumerate(req):
             (a1, a2), (b1, b2) = two(aa), two(ab)
             off, wdt = region[into[0]] if into is not None else region[k]
             off += into[1] if into is not None else 0
@@ -735,7 +752,7 @@ class WgradBatch:
             descs[k] = _WgradDesc(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), P,
                                   a1, b1, part.data_ptr() + 4 * off, ldt,
                                   part.data_ptr() + 4 * (ld + boff) if wb else None, ldt,
-                                  A.shape[0], B.shape[0], a2, b2, wdt, bs(A), bs(B))
+                                  A.shape[0], B.shape[0], a2, b2, wdt, bs(A), bs(B), a_split)
             boff += bsizes[k]
         st = _lib.stream_of(self.device)
         zarr = (ctypes.c_int * len(zs))(*zs)
@@ -744,7 +761,7 @@ class WgradBatch:
         call("nerf_sum_partials", ptr(part), Z, ldt, ptr(total), st)
         flat, bflat = total[:ld], total[ld:]
         out, boff = [], 0
-        for k, (A, B, _, _, wb, _, into) in enumerate(req):
+        for k, (A, B, _, _, wb, _, into, _) in enumerate(req):
             if into is not None:
                 out.append(None)
                 continue
@@ -1031,8 +1048,10 @@ class NerfMLPFn(torch.autograd.Function):
         post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
             "rgb_linear.weight", "rgb_linear.bias", None)
         if heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
+            # d sigma (row 128) keeps its own FP16 split range: rows 128.. at
+            # max |d sigma|, not at max |d hv| (a much larger d hv would flush it)
             post[wb.add(rows_of(HX, 0, 129), V, (dmax[10:11], dmax[12:13]),
-                        (amax[7:8], amax[10:11]), with_bias=True)] = (
+                        (amax[7:8], amax[10:11]), with_bias=True, a_split=128)] = (
                 "views_G", "views_GA_bias", None)
         elif v_h7:   # G = d_hv [h7; enc]^T: both the views and the feature gradients (below)
             post[wb.add(d_hv, V, dmax[10:11], (amax[7:8], amax[10:11]),

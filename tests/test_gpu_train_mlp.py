@@ -88,6 +88,37 @@ def test_x3_train_mlp_forward_backward_match_torch(dev, P, fused, monkeypatch):
         assert _rel(a, b) < 1e-4, (name, _rel(a, b))
 
 
+@pytest.mark.parametrize("P", [1024, 1000])
+def test_tiny_sigma_gradient_keeps_its_split_range(dev, P, monkeypatch):
+    """The fused forward + backward read the alpha head's gradient off the
+    views layer's weight-gradient tile: its A operand is [d hv; d sigma] (d sigma
+    at row 128). With one FP16 split range for both (the max of the two), a
+    d sigma far below d hv would split into denormal / flushed halves; row 128
+    takes its own range (NerfWgradDesc.a2_row; the unaligned P = 1000 goes
+    through the per-block fallback). d sigma scaled by 2^-30: every gradient,
+    alpha_linear's included, within 1e-4 of torch FP32 autograd of the
+    reference module (network.py:49-74)."""
+    from nerfhip import train_mlp
+    from nerfhip.train import freq_encode
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    monkeypatch.setattr(train_mlp, "FUSED_FORWARD", True)
+    monkeypatch.setattr(train_mlp, "FUSED_BACKWARD", True)
+    m = _model(dev)
+    pts, dirs = _inputs(dev, P)
+    d_raw = torch.randn((P, 4), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    d_raw[:, 3] *= 2.0 ** -30
+    d_raw[_relu_edge_samples(m, pts, dirs)] = 0.0
+    x = pts.clone().requires_grad_(True)
+    ref = m(torch.cat([freq_encode(x, 10), freq_encode(dirs, 4)], -1))
+    ref_grads = torch.autograd.grad(ref, [x] + mlp_params(m), d_raw)
+    y = pts.clone().requires_grad_(True)
+    out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+    got = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
+    errs = {name: _rel(a, b) for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads)}
+    assert errs["alpha_linear.weight"] < 1e-4 and errs["alpha_linear.bias"] < 1e-4, errs
+    assert max(errs.values()) < 1e-4, errs
+
+
 def test_x3_layer_kernel_matches_matmul(dev):
     """One nerf_x3_layer launch per supported shape: bias + ReLU + mask + rank-1."""
     from nerfhip.train_mlp import _layer, pack_x3_matrix
