@@ -1,6 +1,7 @@
 #!/bin/bash
 # self-split weight-gradient kernel vs round 4's per-wave split (make variant
-# V=ss0 VFLAGS=-DNERF_WGRAD_SELFSPLIT=0): results bit for bit, launch times,
+# V=ss0 VFLAGS=-DNERF_WGRAD_SELFSPLIT=0 at commit 5e5efee; the form is removed
+# since): results bit for bit, launch times,
 # C3 step times interleaved, then the training-MLP tests on the shipped build
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
