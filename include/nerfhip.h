@@ -390,6 +390,14 @@ int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int
  * exponent of the matrix whose amax slot is table[i] - 1, or 0 (table[i] 0). */
 int nerf_x3_pack(const void* descs, int n, const void* heads, int n_heads, nerf_stream_t stream);
 
+/* VR:310-314, :1098-1103 (raw_noise_std > 0): out[i] = raw[i] with its density
+ * logit (.w) plus noise[i] -- the caller's torch.randn(...) * raw_noise_std in the
+ * reference's draw order; raw / out float4 [count], noise [count]; out may be
+ * raw. The composites then read out (the ESS grid update keeps the raw without
+ * noise, as VR:1150-1153 does). */
+int nerf_add_sigma_noise(const float* raw, const float* noise, int64_t count, float* out,
+                         nerf_stream_t stream);
+
 /* VR:286-357: alpha compositing of raw[n*S][4] along z (row stride z_stride).
  * Reductions follow torch's CPU float32 summation order.
  * Outputs rgb[n][3], disp/acc/depth[n]; weights[n][S] optional (NULL). */

@@ -1075,6 +1075,33 @@ int nerf_sample_coarse(const float* z_base, const float* t_rand, int64_t n, int 
   return check_launch("coarse_kernel");
 }
 
+// VR:310-314 / :1098-1103 (raw_noise_std > 0): the density logit of every
+// sample plus its noise (torch.randn * raw_noise_std, drawn by the caller in
+// the reference's order), one FP32 add as `raw[..., 3] + noise`; rgb logits
+// copied. The composite kernels then read the noisy raw.
+__global__ __launch_bounds__(256) void add_sigma_noise_kernel(const float4* __restrict__ raw,
+                                                              const float* __restrict__ noise,
+                                                              int64_t count,
+                                                              float4* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 v = raw[i];
+    v.w = v.w + noise[i];
+    out[i] = v;
+  }
+}
+
+int nerf_add_sigma_noise(const float* raw, const float* noise, int64_t count, float* out,
+                         nerf_stream_t stream) {
+  NERF_REQUIRE(raw && noise && out, "nerf_add_sigma_noise: null pointer");
+  NERF_REQUIRE(count >= 0, "nerf_add_sigma_noise: bad size");
+  if (count == 0) return 0;
+  const int64_t blocks = std::min<int64_t>(cdiv(count, 256), 256 * 64);
+  hipLaunchKernelGGL(add_sigma_noise_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     as_stream(stream), (const float4*)raw, noise, count, (float4*)out);
+  return check_launch("add_sigma_noise_kernel");
+}
+
 int nerf_composite(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
                    int64_t n, int S, int white_bkgd, float* rgb, float* disp, float* acc,
                    float* depth, float* weights, nerf_stream_t stream) {

@@ -39,15 +39,30 @@ def reference_draws(n, S, NI, perturb, draw_u, device):
     :1080-1085) and then, when ``draw_u`` (``self.net.training``, VR:247-249), the
     fine-sampling u [m, NI]. Returns (t_rand [n, S] | None, u [n, NI] | None), so
     a whole-frame pass consumes the same random stream as the chunk loop."""
-    tr, uu = [], []
+    return reference_draws_noise(n, S, NI, perturb, draw_u, device, 0.0)[:2]
+
+
+def reference_draws_noise(n, S, NI, perturb, draw_u, device, noise_std):
+    """reference_draws plus, when ``noise_std > 0``, the density noise of the two
+    composites of every chunk (``torch.randn(raw[..., 3].shape) * raw_noise_std``,
+    VR:310-314 / :1098-1103), in the chunk's order: t_rand, the coarse noise
+    [m, S], u, the fine noise [m, S + NI]. Returns (t_rand, u, noise_c [n, S],
+    noise_f [n, S + NI]), each None when not drawn."""
+    tr, uu, nc, nf = [], [], [], []
     for c0 in range(0, n, REF_CHUNK):
         m = min(REF_CHUNK, n - c0)
         if perturb > 0:
             tr.append(torch.rand((m, S), device=device))
+        if noise_std > 0:
+            nc.append(torch.randn((m, S), device=device) * noise_std)
         if draw_u and NI > 0:
             uu.append(torch.rand((m, NI), device=device))
-    return (torch.cat(tr).contiguous() if tr else None,
-            torch.cat(uu).contiguous() if uu else None)
+        if noise_std > 0 and NI > 0:
+            nf.append(torch.randn((m, S + NI), device=device) * noise_std)
+
+    def cat(x):
+        return torch.cat(x).contiguous() if x else None
+    return cat(tr), cat(uu), cat(nc), cat(nf)
 
 
 MLP_KERNELS = {"fp32": ("nerf_mlp_forward", pack_mlp),
@@ -199,11 +214,18 @@ class NerfPipeline:
         t.append((name, e0, e1, nbytes))
         return r
 
-    def composite(self, raw, z, z_stride, rays_d, n, S, out, off, need_weights=True):
+    def composite(self, raw, z, z_stride, rays_d, n, S, out, off, need_weights=True, noise=None):
         """Writes rgb/disp/acc/depth rows [off, off+n) of `out`; returns the weights
-        [n, S] (or None when not needed: the kernel then skips writing them)."""
+        [n, S] (or None when not needed: the kernel then skips writing them).
+        noise [n, S]: added to the density logits first (raw_noise_std > 0,
+        VR:310-314 / :1098-1103; `raw` itself is left as it is)."""
         w = (torch.empty((n, S), device=self.device, dtype=torch.float32)
              if need_weights else None)
+        if noise is not None:
+            noisy = torch.empty_like(raw)
+            call("nerf_add_sigma_noise", ptr(raw), ptr(noise), n * S, ptr(noisy),
+                 _lib.stream_of(self.device))
+            raw = noisy
         rgb, disp, acc, depth = out
         args = (ptr(raw), ptr(z), z_stride, ptr(rays_d), n, S, int(self.white_bkgd))
         tail = (ptr(rgb[off:]), ptr(disp[off:]), ptr(acc[off:]), ptr(depth[off:]), ptr(w),
@@ -221,11 +243,14 @@ class NerfPipeline:
         return w
 
     # ------------------------------------------------------------------ rays
-    def render_rays(self, rays_o, rays_d, t_rand=None, u=None, outputs=None, off=0):
+    def render_rays(self, rays_o, rays_d, t_rand=None, u=None, outputs=None, off=0, noise=None):
         """Render n rays (rows of rays_o/rays_d, [n,3] float32 on the device).
 
         With ERT/ESS the rays must start on a 2048-ray chunk boundary of the
-        reference's chunking (VR:147). Returns the per-ray output buffers.
+        reference's chunking (VR:147). noise = (coarse [n, S], fine [n, S+NI]):
+        the density noise of raw_noise_std > 0 (reference_draws_noise); the ERT
+        sample compaction is off then (its termination test reads raw without
+        noise). Returns the per-ray output buffers.
         """
         n = rays_o.shape[0]
         S, NI = self.N_samples, self.N_importance
@@ -246,6 +271,7 @@ class NerfPipeline:
             counter0 = self.grid_update_counter
             ro, rd = rays_o[p:p + m], rays_d[p:p + m]
             tr = None if t_rand is None else t_rand[p:p + m]
+            nz_c, nz_f = (None, None) if noise is None else (noise[0][p:p + m], noise[1][p:p + m])
             if self.enable_ess:
                 if self.grid is None:
                     raise _lib.NerfHipError("ESS enabled but no occupancy grid set")
@@ -260,8 +286,8 @@ class NerfPipeline:
                 zs = S
             else:
                 z, zs = self.z_base, 0                     # one shared row (expand)
-            raw = self._pass_mlp(self.coarse, ro, rd, z, zs, m, S)
-            w = self.composite(raw, z, zs, rd, m, S, outputs["coarse"], off + p)
+            raw = self._pass_mlp(self.coarse, ro, rd, z, zs, m, S, compact=noise is None)
+            w = self.composite(raw, z, zs, rd, m, S, outputs["coarse"], off + p, noise=nz_c)
             self._grid_updates(0, counter0, rd, z, zs, raw, w, m, S)
             if NI > 0:
                 zall = torch.empty((m, S + NI), device=dev, dtype=torch.float32)
@@ -276,9 +302,10 @@ class NerfPipeline:
                 del raw, w
                 if self.capture_zall is not None:
                     self.capture_zall.append(zall.clone())
-                raw_f = self._pass_mlp(self.fine, ro, rd, zall, S + NI, m, S + NI)
+                raw_f = self._pass_mlp(self.fine, ro, rd, zall, S + NI, m, S + NI,
+                                       compact=noise is None)
                 w_f = self.composite(raw_f, zall, S + NI, rd, m, S + NI, outputs["fine"], off + p,
-                                     need_weights=self.enable_ert and self.enable_ess)
+                                     need_weights=self.enable_ert and self.enable_ess, noise=nz_f)
                 self._grid_updates(1, counter0, rd, zall, S + NI, raw_f, w_f, m, S + NI)
                 del raw_f, w_f, zall
             if self.enable_ert:       # _raw2outputs_with_ert counts its calls (VR:1157)
@@ -286,8 +313,8 @@ class NerfPipeline:
             p += m
         return outputs
 
-    def _pass_mlp(self, packed, ro, rd, z, zs, m, S):
-        if self.enable_ert and self.ert_compaction and self.mlp_precision == "f16x3":
+    def _pass_mlp(self, packed, ro, rd, z, zs, m, S, compact=True):
+        if compact and self.enable_ert and self.ert_compaction and self.mlp_precision == "f16x3":
             return self.mlp_ert(packed, ro, rd, z, zs, m, S)
         return self.mlp(packed, ro, rd, z, zs, m, S)
 
@@ -505,12 +532,13 @@ class NerfPipeline:
         self.grid_update_counter = cf + per * total
         return maps_dict(outputs) if chunks else {}
 
-    def render_image(self, H, W, pose, K, t_rand=None, u=None, p0=0, n=None):
+    def render_image(self, H, W, pose, K, t_rand=None, u=None, p0=0, n=None, noise=None):
         """Render pixels [p0, p0+n) of an H x W image; returns the reference's map dict
-        (``rgb_map_0, disp_map_0, acc_map_0, depth_map_0`` + fine maps), flat per pixel."""
+        (``rgb_map_0, disp_map_0, acc_map_0, depth_map_0`` + fine maps), flat per pixel.
+        noise: (coarse, fine) density noise of these pixels (render_rays)."""
         n = H * W - p0 if n is None else n
         rays_o, rays_d = self.camera_rays(H, W, pose, K, p0, n)
-        out = self.render_rays(rays_o, rays_d, t_rand=t_rand, u=u)
+        out = self.render_rays(rays_o, rays_d, t_rand=t_rand, u=u, noise=noise)
         return maps_dict(out)
 
 

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import call, ptr
-from .render import REF_CHUNK, coarse_depth_table, reference_draws
+from .render import REF_CHUNK, coarse_depth_table, reference_draws_noise
 
 XYZ_FREQS, DIR_FREQS = 10, 4
 
@@ -117,7 +117,7 @@ def composite_ert(raw, z, rays_d, thr, white_bkgd, chunk=2048):
 
 def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=query,
                  detach_fine_samples=False, composite_fn=None, on_composite=None,
-                 hip_ops=False):
+                 hip_ops=False, noise=None):
     """The differentiable part of a training step (VR:164-194): coarse depths z
     [n, S] (no gradient) -> coarse maps, importance samples from the coarse
     weights (u [n, N_importance]), fine maps. fine=None: coarse only.
@@ -130,7 +130,10 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
     _raw2outputs (e.g. composite_ert); on_composite(kind, z, raw, weights) is
     called after each composite (kind 0 coarse, 1 fine: the ESS grid hook).
     hip_ops: compositing (unless composite_fn is given) and importance sampling
-    + merge on the HIP kernels of train_ops (no host syncs: graph-capturable)."""
+    + merge on the HIP kernels of train_ops (no host syncs: graph-capturable).
+    noise = (coarse [n, S], fine [n, S + NI]): density noise (raw_noise_std > 0,
+    VR:310-314) added to raw before each composite; on_composite sees raw without
+    it (the reference's grid update reads raw, VR:1150-1153)."""
     if composite_fn is None and hip_ops:
         from .train_ops import composite_hip
 
@@ -147,8 +150,13 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
         if rays_q is not None:
             return rays_q(model, rays_o, rays_d, zz)
         return query_fn(model, rays_o[:, None, :] + rays_d[:, None, :] * zz[..., None], rays_d)
+    def noisy(raw, k):
+        if noise is None:
+            return raw
+        from .train_ops import add_sigma_noise
+        return add_sigma_noise(raw, noise[k])
     raw = q(coarse, z)
-    rgb0, disp0, acc0, w, depth0 = composite_fn(raw, z, rays_d)
+    rgb0, disp0, acc0, w, depth0 = composite_fn(noisy(raw, 0), z, rays_d)
     if on_composite is not None:
         on_composite(0, z, raw, w)
     out = {"rgb_map_0": rgb0, "disp_map_0": disp0, "acc_map_0": acc0, "depth_map_0": depth0}
@@ -163,7 +171,7 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
                 zf = zf.detach()
             z2, _ = torch.sort(torch.cat([z, zf], -1), -1)
         raw2 = q(fine, z2)
-        rgb, disp, acc, w2, depth = composite_fn(raw2, z2, rays_d)
+        rgb, disp, acc, w2, depth = composite_fn(noisy(raw2, 1), z2, rays_d)
         if on_composite is not None:
             on_composite(1, z2, raw2, w2)
         out.update(rgb_map=rgb, disp_map=disp, acc_map=acc, depth_map=depth)
@@ -171,7 +179,7 @@ def render_train(coarse, fine, rays_o, rays_d, z, u, white_bkgd=True, query_fn=q
 
 
 def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
-                      detach_fine_samples=False):
+                      detach_fine_samples=False, noise_std=0.0):
     """The reference's training-mode ``_render_pytorch`` over a ray block
     (VR:145-216 with ``self.net.training``): per 2048-ray chunk, in the
     reference's order, the perturb draw t_rand [m, S] (VR:228-235 / ESS
@@ -181,7 +189,9 @@ def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
     with its chunk rule (composite_ert), the ESS grid self-update and call
     counter of VR:1147-1157 on detached values, passes cut after a
     grid-updating chunk as in NerfPipeline.render_rays. ``pipe`` is the
-    NerfPipeline holding the configuration, tables, grid and counter."""
+    NerfPipeline holding the configuration, tables, grid and counter.
+    noise_std > 0 (raw_noise_std): the composites' density noise drawn in the
+    reference's chunk order (render.reference_draws_noise)."""
     n = rays_o.shape[0]
     S, NI = pipe.N_samples, pipe.N_importance
     dev = pipe.device
@@ -193,7 +203,7 @@ def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
         if pipe.enable_ess and pipe.enable_ert:
             m = pipe._ess_phase_len(m)
         ro, rd = rays_o[p:p + m], rays_d[p:p + m]
-        t_rand, u = reference_draws(m, S, NI, perturb, True, dev)
+        t_rand, u, nc, nf = reference_draws_noise(m, S, NI, perturb, True, dev, noise_std)
         z = torch.empty((m, S), device=dev, dtype=torch.float32)
         if pipe.enable_ess:
             if pipe.grid is None:
@@ -221,7 +231,8 @@ def render_rays_train(pipe, coarse, fine, rays_o, rays_d, perturb, query_fn,
                 return composite(raw, zz, rdd, pipe.white_bkgd)
         outs.append(render_train(coarse, fine if NI > 0 else None, ro, rd, z, u,
                                  pipe.white_bkgd, query_fn, detach_fine_samples,
-                                 comp if pipe.enable_ert else None, hook, hip_ops=True))
+                                 comp if pipe.enable_ert else None, hook, hip_ops=True,
+                                 noise=(nc, nf) if noise_std > 0 else None))
         if pipe.enable_ert:
             pipe.grid_update_counter = counter0 + pipe._calls_per_chunk() * -(-m // REF_CHUNK)
         p += m

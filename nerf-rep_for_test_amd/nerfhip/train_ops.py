@@ -11,7 +11,10 @@ torch-op versions.
   (the reference does not detach the fine samples, so the fine loss reaches the
   coarse network through them).
 
-Neither needs a host synchronisation, so a step built from them can be
+* ``add_sigma_noise(raw, noise)``: raw with ``noise`` added to the density
+  logit (raw_noise_std > 0, VR:310-314 / :1098-1103), gradient passed through.
+
+None needs a host synchronisation, so a step built from them can be
 captured into a HIP graph (``NerfTrainer(graph=True)``).
 """
 from __future__ import annotations
@@ -24,6 +27,27 @@ from ._lib import call, ptr
 
 def _c(t):
     return None if t is None else t.contiguous()
+
+
+class AddSigmaNoiseFn(torch.autograd.Function):
+    """raw [..., 4] with noise [...] added to raw[..., 3] (nerf_add_sigma_noise);
+    d raw = d out (the noise is a constant of the step)."""
+    @staticmethod
+    def forward(ctx, raw, noise):
+        raw_c, nz = raw.detach().contiguous(), noise.detach().contiguous()
+        assert nz.numel() * 4 == raw_c.numel()
+        out = torch.empty_like(raw_c)
+        call("nerf_add_sigma_noise", ptr(raw_c), ptr(nz), nz.numel(), ptr(out),
+             _lib.stream_of(raw.device))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def add_sigma_noise(raw, noise):
+    return AddSigmaNoiseFn.apply(raw, noise)
 
 
 class CompositeFn(torch.autograd.Function):

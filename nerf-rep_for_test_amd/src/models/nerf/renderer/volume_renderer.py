@@ -19,7 +19,7 @@ import torch
 from src.config import cfg
 from nerfhip import _lib
 from nerfhip.paths import spiral_poses
-from nerfhip.render import NerfPipeline, reference_draws
+from nerfhip.render import NerfPipeline, reference_draws_noise
 
 
 class Renderer:
@@ -51,9 +51,6 @@ class Renderer:
         if not self.use_viewdirs:
             raise NotImplementedError("use_viewdirs=False is not on the lego render path")
         self._check_topology()
-        if self.raw_noise_std and float(self.raw_noise_std) > 0:
-            raise NotImplementedError("raw_noise_std > 0 (training-time density noise) "
-                                      "is not implemented in the HIP path")
         self.pipeline = NerfPipeline(
             self.device, N_samples=self.N_samples, N_importance=self.N_importance,
             near=self.near, far=self.far, lindisp=self.lindisp, white_bkgd=self.white_bkgd,
@@ -160,11 +157,16 @@ class Renderer:
         K = torch.as_tensor(batch["intrinsics"]).reshape(-1, 3, 3)[0].float()
         self._sync_weights()
         # the reference's draws in its order: per 2048-ray chunk t_rand (perturb > 0,
-        # also at eval: lego.yaml:22), then u when the net is in training mode
-        t_rand, u = reference_draws(H * W, self.N_samples, self.N_importance,
-                                    float(self.perturb), self.net.training, self.device)
+        # also at eval: lego.yaml:22), the coarse composite's density noise
+        # (raw_noise_std > 0, VR:310-314), u when the net is in training mode, the
+        # fine composite's noise
+        std = float(self.raw_noise_std or 0.0)
+        t_rand, u, nc, nf = reference_draws_noise(H * W, self.N_samples, self.N_importance,
+                                                  float(self.perturb), self.net.training,
+                                                  self.device, std)
+        noise = (nc, nf if nf is not None else nc) if std > 0 else None
         with torch.no_grad():
-            res = self.pipeline.render_image(H, W, pose, K, t_rand=t_rand, u=u)
+            res = self.pipeline.render_image(H, W, pose, K, t_rand=t_rand, u=u, noise=noise)
         out = {}
         for k, v in res.items():
             out[k] = v.view(H, W, 3) if k.startswith("rgb") else v.view(H, W)
@@ -188,7 +190,8 @@ class Renderer:
         qf = query if getattr(cfg, "train_mlp", "x3") == "torch" else query_x3
         res = render_rays_train(self.pipeline, self.coarse_model,
                                 self.fine_model if self.N_importance > 0 else None,
-                                rays_o, rays_d, float(self.perturb), qf)
+                                rays_o, rays_d, float(self.perturb), qf,
+                                noise_std=float(self.raw_noise_std or 0.0))
         return {k: v.view(H, W, 3) if k.startswith("rgb") else v.view(H, W)
                 for k, v in res.items()}
 
@@ -201,7 +204,9 @@ class Renderer:
         return spiral_poses(poses, int(n_frames), n_rots, zrate)
 
     def render_path(self, render_poses, hwf, intrinsics=None, chunk_size=None):
-        """VR:421-509: rgb [N,H,W,3] and disp [N,H,W] of every pose, clipped like the
+        """VR:421-509: rgb [N,H,W,3] and disp [N,H,W] of every pose through
+        render(batch) under no_grad (so perturb / density-noise draws and the ESS
+        grid self-update happen as in the reference's loop), clipped like the
         reference (rgb to [0,1], disp to [0, max]). Errors propagate (the reference
         substitutes black frames)."""
         H, W, focal = hwf
@@ -210,15 +215,17 @@ class Renderer:
             K = np.array([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], np.float32)
         else:
             K = intrinsics.cpu().numpy() if torch.is_tensor(intrinsics) else np.asarray(intrinsics)
-        self._sync_weights()
+        Kt = torch.as_tensor(np.asarray(K, np.float32))[None]
         rgbs, disps = [], []
         for pose in render_poses:
             pose = pose.cpu().numpy() if torch.is_tensor(pose) else np.asarray(pose, np.float32)
+            batch = {"pose": torch.as_tensor(np.asarray(pose, np.float32))[None],
+                     "intrinsics": Kt, "H": H, "W": W}
             with torch.no_grad():
-                res = self.pipeline.render_image(H, W, pose, K)
+                res = self.render(batch)
             key = "rgb_map" if "rgb_map" in res else "rgb_map_0"
-            rgb = res[key].view(H, W, 3).cpu().numpy()
-            disp = res[key.replace("rgb", "disp")].view(H, W).cpu().numpy()
+            rgb = res[key].cpu().numpy()
+            disp = res[key.replace("rgb", "disp")].cpu().numpy()
             mx = np.max(disp)
             rgbs.append(np.clip(rgb, 0, 1))
             disps.append(np.clip(disp, 0, mx if mx > 0 else 1.0))

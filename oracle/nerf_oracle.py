@@ -414,8 +414,16 @@ class RenderConfig:
         del self.__dict__["self"]
 
 
+def add_sigma_noise(raw, noise):
+    """VR:310-314 / :1098-1103: ``raw[..., 3] + noise`` (one float32 add; noise =
+    the reference's torch.randn(...) * raw_noise_std); rgb logits unchanged."""
+    out = raw.astype(F32, copy=True)
+    out[..., 3] = (out[..., 3] + noise.astype(F32)).astype(F32)
+    return out
+
+
 def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
-           grid=None, grid_counter=0, rays=None, return_zall=False):
+           grid=None, grid_counter=0, rays=None, return_zall=False, noise=None):
     """VR:109-216 on the CPU. Returns (dict of maps, final grid_counter).
 
     ``t_rand`` [H*W, N_samples] supplies the stratification draws when
@@ -423,6 +431,9 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
     is the ESS occupancy grid (mutated in place by the reference's update rule).
     ``rays`` = (rays_o, rays_d) overrides the camera (used by sharded tests).
     ``return_zall`` adds ``res["zall"]`` [n, S+NI]: the merged fine depths (VR:183).
+    ``noise`` = (coarse [H*W, S], fine [H*W, S+NI]): raw_noise_std > 0's density
+    noise, added before each composite (VR:310-314); the grid update reads raw
+    without it (VR:1150-1153).
     """
     if rays is None:
         rays_o, rays_d = camera_rays(H, W, pose, K)
@@ -446,17 +457,18 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
         pts = (ro[:, None, :] + rd[:, None, :] * z[:, :, None]).astype(F32)
         raw = query_network(pts, rd, params, "model", cfg.chunk_size)
 
-        def comp(raw_, z_):
+        def comp(raw_, z_, k):
             nonlocal counter
+            rn = raw_ if noise is None else add_sigma_noise(raw_, noise[k][sl])
             if cfg.enable_ert:
-                r = raw2outputs_ert(raw_, z_, rd, cfg.ert_threshold, cfg.white_bkgd)
+                r = raw2outputs_ert(rn, z_, rd, cfg.ert_threshold, cfg.white_bkgd)
                 if cfg.enable_ess and counter % cfg.grid_update_interval == 0:
                     update_grid(grid, rd, z_, raw_, r[3])
                 counter += 1
                 return r
-            return raw2outputs(raw_, z_, rd, cfg.white_bkgd)
+            return raw2outputs(rn, z_, rd, cfg.white_bkgd)
 
-        rgb0, disp0, acc0, w0, depth0 = comp(raw, z)
+        rgb0, disp0, acc0, w0, depth0 = comp(raw, z, 0)
         ret = {"rgb_map_0": rgb0, "disp_map_0": disp0, "acc_map_0": acc0, "depth_map_0": depth0}
         if cfg.N_importance > 0:
             mids = (F32(0.5) * (z[:, 1:] + z[:, :-1])).astype(F32)
@@ -469,7 +481,7 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
             zalls.append(zall)
             pts_f = (ro[:, None, :] + rd[:, None, :] * zall[:, :, None]).astype(F32)
             raw_f = query_network(pts_f, rd, params, "model_fine", cfg.chunk_size)
-            rgb, disp, acc, _, depth = comp(raw_f, zall)
+            rgb, disp, acc, _, depth = comp(raw_f, zall, 1)
             ret.update({"rgb_map": rgb, "disp_map": disp, "acc_map": acc, "depth_map": depth})
         for k, v in ret.items():
             out.setdefault(k, []).append(v)

@@ -86,6 +86,17 @@ FIXTURES = {
     # F5: lego 400^2 camera crop, 64 coarse only
     "f5_c1_crop": dict(H=32, W=32, res=400, x0=184, y0=184, frame=0, w=(0, 2.0, 0.0),
                        cfg=dict(N_importance=0, perturb=0, enable_ess=False, enable_ert=False)),
+    # N1: F2 over two chunks (2048 + 256 rays) with density noise (raw_noise_std 0.5,
+    # VR:310-314): the torch.randn draws of both composites recorded in order.
+    # (n*: not in the f* crop sets -- tests/test_*noise* hold them to their gates)
+    "n1_c2_noise": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                        cfg=dict(N_importance=128, perturb=1, enable_ess=False, enable_ert=False,
+                                 raw_noise_std=0.5)),
+    # N1b: F4b (ESS + ERT, grid self-update, perturb) with density noise (VR:1098-1103)
+    "n1b_ess_ert_noise": dict(H=48, W=48, res=800, x0=376, y0=376, frame=0, w=(0, 3.0, 1.0),
+                              cfg=dict(N_importance=128, perturb=1, enable_ess=True,
+                                       enable_ert=True, ert_threshold=0.01, raw_noise_std=0.5),
+                              grid=dict(seed=4, radius=0.5, noise=0.01), counter=0),
     # F6: ragged 1x7 strip, lindisp
     "f6_ragged_lindisp": dict(H=1, W=7, res=800, x0=396, y0=400, frame=3, w=(2, 2.0, 0.5),
                               cfg=dict(N_importance=128, perturb=0, enable_ess=False,
@@ -109,6 +120,7 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
         if k in spec["cfg"]:
             cfg.task_arg[k] = spec["cfg"][k]
     cfg.task_arg.lindisp = spec["cfg"].get("lindisp", False)
+    cfg.task_arg.raw_noise_std = spec["cfg"].get("raw_noise_std", 0.0)
     for k in ("enable_ess", "enable_ert", "ert_threshold"):
         if k in spec["cfg"]:
             cfg[k] = spec["cfg"][k]
@@ -129,11 +141,21 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
     pose, K = _camera(spec, frames, angle)
 
     draws = []
-    orig_rand = torch.rand
+    order = []   # ("rand" | "randn", shape) of every draw, in the reference's order
+    orig_rand, orig_randn = torch.rand, torch.randn
 
     def rec_rand(*a, **kw):
         t = orig_rand(*a, **kw)
         draws.append(t.detach().clone().numpy())
+        order.append(("rand",) + tuple(t.shape))
+        return t
+
+    noise = []
+
+    def rec_randn(*a, **kw):
+        t = orig_randn(*a, **kw)
+        noise.append(t.detach().clone().numpy())
+        order.append(("randn",) + tuple(t.shape))
         return t
 
     inter = {}
@@ -182,12 +204,12 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
     rend._query_network = rec_q
     batch = {"H": spec["H"], "W": spec["W"], "pose": torch.from_numpy(pose)[None],
              "intrinsics": torch.from_numpy(K)[None]}
-    torch.rand = rec_rand
+    torch.rand, torch.randn = rec_rand, rec_randn
     try:
         with torch.no_grad():
             out = rend.render(batch)
     finally:
-        torch.rand = orig_rand
+        torch.rand, torch.randn = orig_rand, orig_randn
     n = spec["H"] * spec["W"]
     if ZALL_ONLY:
         old = np.load(os.path.join(OUT, name + ".npz"))
@@ -217,6 +239,14 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
         # one [chunk, N_samples] draw per 2048-ray chunk (volume_renderer.py:233, :1083)
         coarse = [d for d in draws if d.ndim == 2 and d.shape[1] == rec["N_samples"]]
         rec["t_rand"] = np.concatenate(coarse, 0)[:n]
+    if noise:
+        # the unscaled torch.randn draws (VR:312, :1101; raw_noise_std multiplies them):
+        # per chunk one [m, N_samples] (coarse composite) and one [m, S + NI] (fine)
+        rec["raw_noise_std"] = float(cfg.task_arg.raw_noise_std)
+        rec["noise_c"] = np.concatenate([d for d in noise if d.shape[1] == rec["N_samples"]], 0)
+        if rec["N_importance"] > 0:
+            rec["noise_f"] = np.concatenate([d for d in noise if d.shape[1] != rec["N_samples"]], 0)
+        rec["draw_order"] = np.array([f"{o[0]}:{o[1]}x{o[2]}" for o in order])
     for k, v in out.items():
         rec["out_" + k] = v.numpy()
     for k, v in inter.items():

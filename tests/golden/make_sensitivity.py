@@ -113,6 +113,7 @@ def _render(torch, make_occupancy_grid, load_into_network, spec, cfg, Network, v
         if k in spec["cfg"]:
             cfg.task_arg[k] = spec["cfg"][k]
     cfg.task_arg.lindisp = spec["cfg"].get("lindisp", False)
+    cfg.task_arg.raw_noise_std = spec["cfg"].get("raw_noise_std", 0.0)
     for k in ("enable_ess", "enable_ert", "ert_threshold"):
         if k in spec["cfg"]:
             cfg[k] = spec["cfg"][k]
