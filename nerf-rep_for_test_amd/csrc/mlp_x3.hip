@@ -486,6 +486,9 @@ struct ActStore {
     const unsigned vo = lane_off();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+#if NERF_ABL_NOSTORE == 3   // timing-only: half the row stores issued (wrong results)
+      if (r >= 2) continue;
+#endif
       st32(v[r], vo, (int)(2 * G * ts + r * rstr));
       st32(v[4 + r], vo, (int)((2 * G + 1) * ts + r * rstr));
     }

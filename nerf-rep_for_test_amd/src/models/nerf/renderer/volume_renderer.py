@@ -49,7 +49,12 @@ class Renderer:
         self.cuda_blocks = getattr(cfg, "cuda_blocks", 128)
         self.cuda_threads = getattr(cfg, "cuda_threads", 256)
         if not self.use_viewdirs:
-            raise NotImplementedError("use_viewdirs=False is not on the lego render path")
+            # the reference cannot render it either: its _query_network (VR:270-284)
+            # hands NeRF.forward the 63 xyz-encoding columns alone, which splits them
+            # as 63 + 27 (network.py:49-51) and raises a RuntimeError
+            raise NotImplementedError("use_viewdirs=False: the reference's own NeRF.forward "
+                                      "cannot run it (network.py:49-51 splits 63 + 27 columns "
+                                      "off a 63-column input)")
         self._check_topology()
         self.pipeline = NerfPipeline(
             self.device, N_samples=self.N_samples, N_importance=self.N_importance,
