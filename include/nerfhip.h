@@ -390,6 +390,14 @@ int nerf_freq_encode_fm_backward_dz(const float* d_enc, const float* d_enc2, int
  * exponent of the matrix whose amax slot is table[i] - 1, or 0 (table[i] 0). */
 int nerf_x3_pack(const void* descs, int n, const void* heads, int n_heads, nerf_stream_t stream);
 
+/* NET:9-74 for network topologies other than lego's (the fused MLP kernels'
+ * one): one nn.Linear (+ ReLU when relu != 0) in FP32 over feature-major
+ * activations, Y[m * sym + p * syp] = act(b[m] + sum_k W[m * K + k] X[k * ldx + p])
+ * for m < M, p < P; b nullable; the k sum in ascending order. Used layer by
+ * layer by nerfhip.generic_mlp. */
+int nerf_linear_fm(const float* W, const float* b, const float* X, int64_t ldx, int K, int64_t P,
+                   int M, int relu, float* Y, int64_t sym, int64_t syp, nerf_stream_t stream);
+
 /* VR:310-314, :1098-1103 (raw_noise_std > 0): out[i] = raw[i] with its density
  * logit (.w) plus noise[i] -- the caller's torch.randn(...) * raw_noise_std in the
  * reference's draw order; raw / out float4 [count], noise [count]; out may be

@@ -60,6 +60,7 @@ SIGNATURES = {
                                              _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_add_sigma_noise": (_I, [_P, _P, _I64, _P, _S]),
+    "nerf_linear_fm": (_I, [_P, _P, _P, _I64, _I, _I64, _I, _I, _P, _I64, _I64, _S]),
     "nerf_composite_ert_workspace": (_SZ, [_I64, _I]),
     "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _P,
                                 _S]),

@@ -121,8 +121,14 @@ class NerfPipeline:
 
     # ------------------------------------------------------------------ weights
     def set_weights(self, params, coarse_prefix="model", fine_prefix="model_fine"):
-        """params: name -> tensor/array (reference state_dict names)."""
+        """params: name -> tensor/array (reference state_dict names). Lego's
+        topology (8 x 256, skip 4, L = 10 / 4) is packed for the fused MLP kernels;
+        any other runs layer by layer (nerfhip.generic_mlp, FP32)."""
+        from .generic_mlp import LEGO, GenericMLP, topology
+
         def up(prefix):
+            if topology(params, prefix) != LEGO:
+                return GenericMLP(params, prefix, self.device)
             sl, hd = MLP_KERNELS[self.mlp_precision][1](params, prefix)
             return (torch.from_numpy(sl).to(self.device), torch.from_numpy(hd).to(self.device))
         self.coarse = up(coarse_prefix)
@@ -151,6 +157,8 @@ class NerfPipeline:
         return n * S * 16 + n * 24 + (n * S if z_stride else S) * 4 + cls.MLP_WEIGHT_BYTES
 
     def mlp(self, packed, rays_o, rays_d, z, z_stride, n, S):
+        if not isinstance(packed, tuple):   # another topology: the layer-by-layer MLP
+            return packed.forward(rays_o, rays_d, z, z_stride, n, S)
         raw = torch.empty((n * S, 4), device=self.device, dtype=torch.float32)
         t = self.timer
         if t is not None:
@@ -314,7 +322,8 @@ class NerfPipeline:
         return outputs
 
     def _pass_mlp(self, packed, ro, rd, z, zs, m, S, compact=True):
-        if compact and self.enable_ert and self.ert_compaction and self.mlp_precision == "f16x3":
+        if (compact and self.enable_ert and self.ert_compaction and self.mlp_precision == "f16x3"
+                and isinstance(packed, tuple)):
             return self.mlp_ert(packed, ro, rd, z, zs, m, S)
         return self.mlp(packed, ro, rd, z, zs, m, S)
 

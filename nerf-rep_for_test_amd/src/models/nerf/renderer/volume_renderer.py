@@ -72,31 +72,19 @@ class Renderer:
             self._initialize_occupancy_grid()
 
     def _check_topology(self):
-        """The HIP kernels implement exactly the lego network (lego.yaml:29-44):
-        xyz / dir frequency encodings with L = 10 / 4 (63 / 27 inputs), 8 x 256
-        layers with the skip after layer 4, a 128-wide views layer. Anything else
-        is refused here rather than packed wrongly."""
-        from nerfhip.synthetic import layer_shapes
-        net_cfg = cfg.get("network", {}) if hasattr(cfg, "get") else {}
-        want = {"nerf": {"W": 256, "D": 8, "skips": [4]}, "xyz_encoder": {"freq": 10},
-                "dir_encoder": {"freq": 4}}
-        for blk, keys in want.items():
-            got = net_cfg.get(blk, {}) if hasattr(net_cfg, "get") else {}
-            for k, v in keys.items():
-                if k not in got:
-                    continue
-                g = list(got[k]) if isinstance(v, list) else got[k]
-                if g != v:
-                    raise NotImplementedError(f"cfg.network.{blk}.{k}={got[k]!r}: the HIP "
-                                              f"kernels implement {v!r} only")
+        """Both networks must be NeRF modules of the reference's kind (network.py:9-43,
+        use_viewdirs=True) with the same topology. Lego's (8 x 256, skip after
+        layer 4, L = 10 / 4 encodings, lego.yaml:29-44) runs on the fused MLP
+        kernels; any other D / W / skips / encoding widths on the layer-by-layer
+        FP32 path (nerfhip.generic_mlp), and training then uses the torch MLP back end."""
+        from nerfhip.generic_mlp import LEGO, topology
+        tops = []
         for prefix, mod in (("model", self.coarse_model), ("model_fine", self.fine_model)):
-            sd = mod.state_dict()
-            for name, fout, fin in layer_shapes(prefix):
-                w = sd.get(name[len(prefix) + 1:] + ".weight")
-                if w is None or tuple(w.shape) != (fout, fin):
-                    raise NotImplementedError(
-                        f"{name}.weight: shape {None if w is None else tuple(w.shape)} != "
-                        f"{(fout, fin)} (the lego 8x256 topology the HIP kernels implement)")
+            sd = {f"{prefix}.{k}": v for k, v in mod.state_dict().items()}
+            tops.append(topology(sd, prefix))
+        if self.N_importance > 0 and tops[0] != tops[1]:
+            raise NotImplementedError(f"coarse {tops[0]} and fine {tops[1]} topologies differ")
+        self.lego_topology = tops[0] == LEGO
 
     # ------------------------------------------------------------- ESS state
     def _initialize_occupancy_grid(self):
@@ -192,7 +180,8 @@ class Renderer:
         pose = torch.as_tensor(batch["pose"]).reshape(-1, 4, 4)[0].float()
         K = torch.as_tensor(batch["intrinsics"]).reshape(-1, 3, 3)[0].float()
         rays_o, rays_d = self.pipeline.camera_rays(H, W, pose, K)
-        qf = query if getattr(cfg, "train_mlp", "x3") == "torch" else query_x3
+        qf = (query if getattr(cfg, "train_mlp", "x3") == "torch" or not self.lego_topology
+              else query_x3)
         res = render_rays_train(self.pipeline, self.coarse_model,
                                 self.fine_model if self.N_importance > 0 else None,
                                 rays_o, rays_d, float(self.perturb), qf,

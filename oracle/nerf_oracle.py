@@ -299,9 +299,26 @@ def _lin(x, p, name, relu):
     return np.maximum(y, F32(0.0)) if relu else y
 
 
-def nerf_mlp(x: np.ndarray, p, prefix: str, skips=(4,), D=8) -> np.ndarray:
-    """NET:49-74 (use_viewdirs=True): returns raw [P,4] = (rgb logits, sigma raw)."""
-    pts, views = x[:, :63], x[:, 63:]
+def topology(p, prefix):
+    """(D, W, skips, L_xyz, L_dir) of a NeRF state dict (NET:9-43): D from the
+    pts_linears present, skips from the layers whose input is [encoding | h]."""
+    D = 0
+    while f"{prefix}.pts_linears.{D}.weight" in p:
+        D += 1
+    W, in_x = p[f"{prefix}.pts_linears.0.weight"].shape
+    skips = tuple(i for i in range(D - 1)
+                  if p[f"{prefix}.pts_linears.{i + 1}.weight"].shape[1] == W + in_x)
+    in_v = p[f"{prefix}.views_linears.0.weight"].shape[1] - W
+    return D, W, skips, (in_x - 3) // 6, (in_v - 3) // 6
+
+
+def nerf_mlp(x: np.ndarray, p, prefix: str, skips=None, D=None) -> np.ndarray:
+    """NET:49-74 (use_viewdirs=True): returns raw [P,4] = (rgb logits, sigma raw).
+    The topology (D, skips, encoding widths) from the state dict (lego: 8, (4,))."""
+    D0, _, skips0, lx, _ = topology(p, prefix)
+    D = D0 if D is None else D
+    skips = skips0 if skips is None else skips
+    pts, views = x[:, :3 + 6 * lx], x[:, 3 + 6 * lx:]
     h = pts
     for i in range(D):
         h = _lin(h, p, f"{prefix}.pts_linears.{i}", True)
@@ -315,12 +332,13 @@ def nerf_mlp(x: np.ndarray, p, prefix: str, skips=(4,), D=8) -> np.ndarray:
 
 
 def query_network(pts, viewdirs, p, prefix, chunk=4096):
-    """VR:270-284: embed xyz (L=10) and dirs (L=4), 4096-point MLP chunks."""
+    """VR:270-284: embed xyz (lego: L=10) and dirs (L=4), 4096-point MLP chunks."""
     n, s, _ = pts.shape
+    _, _, _, lx, ld = topology(p, prefix)
     flat = pts.reshape(-1, 3)
-    e = embed(flat, 10)
+    e = embed(flat, lx)
     d = np.broadcast_to(viewdirs[:, None, :], pts.shape).reshape(-1, 3)
-    e = np.concatenate([e, embed(d, 4)], -1)
+    e = np.concatenate([e, embed(d, ld)], -1)
     out = np.concatenate([nerf_mlp(e[i:i + chunk], p, prefix)
                           for i in range(0, e.shape[0], chunk)], 0)
     return out.reshape(n, s, 4)

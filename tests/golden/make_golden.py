@@ -97,6 +97,12 @@ FIXTURES = {
                               cfg=dict(N_importance=128, perturb=1, enable_ess=True,
                                        enable_ert=True, ert_threshold=0.01, raw_noise_std=0.5),
                               grid=dict(seed=4, radius=0.5, noise=0.01), counter=0),
+    # G1: another topology (network.py:9-43 with D 6, W 128, skips [2, 3], L 8 / 3
+    # encodings; the reference's own initialisation under torch.manual_seed(7)),
+    # 64 + 64 samples. (g*: not in the f* crop sets -- test_generic_mlp.py)
+    "g1_generic": dict(H=32, W=32, res=800, x0=384, y0=384, frame=0, w=None,
+                       net=dict(D=6, W=128, skips=[2, 3], xyz_freq=8, dir_freq=3, seed=7),
+                       cfg=dict(N_importance=64, perturb=0, enable_ess=False, enable_ert=False)),
     # F6: ragged 1x7 strip, lindisp
     "f6_ragged_lindisp": dict(H=1, W=7, res=800, x0=396, y0=400, frame=3, w=(2, 2.0, 0.5),
                               cfg=dict(N_importance=128, perturb=0, enable_ess=False,
@@ -124,10 +130,25 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
     for k in ("enable_ess", "enable_ert", "ert_threshold"):
         if k in spec["cfg"]:
             cfg[k] = spec["cfg"][k]
-    seed, gain, ab = spec["w"]
-    params = make_params(seed, gain, ab)
-    net = Network()
-    load_into_network(net, params)
+    saved = None
+    if spec.get("net"):   # another topology, the reference's own initialisation
+        nt = spec["net"]
+        saved = (cfg.network.nerf.D, cfg.network.nerf.W, list(cfg.network.nerf.skips),
+                 cfg.network.xyz_encoder.freq, cfg.network.dir_encoder.freq)
+        cfg.network.nerf.D, cfg.network.nerf.W = nt["D"], nt["W"]
+        cfg.network.nerf.skips = list(nt["skips"])
+        cfg.network.xyz_encoder.freq, cfg.network.dir_encoder.freq = nt["xyz_freq"], nt["dir_freq"]
+        torch.manual_seed(nt["seed"])
+        net = Network()
+        params = {f"{pre}.{k}": v.detach().numpy().copy()
+                  for pre, mod in (("model", net.model), ("model_fine", net.model_fine))
+                  for k, v in mod.state_dict().items()}
+        seed = gain = ab = None
+    else:
+        seed, gain, ab = spec["w"]
+        params = make_params(seed, gain, ab)
+        net = Network()
+        load_into_network(net, params)
     net.eval()
     torch.manual_seed(1234)
     rend = vr.Renderer(net)
@@ -211,6 +232,9 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
     finally:
         torch.rand, torch.randn = orig_rand, orig_randn
     n = spec["H"] * spec["W"]
+    if saved is not None:
+        (cfg.network.nerf.D, cfg.network.nerf.W, cfg.network.nerf.skips,
+         cfg.network.xyz_encoder.freq, cfg.network.dir_encoder.freq) = saved
     if ZALL_ONLY:
         old = np.load(os.path.join(OUT, name + ".npz"))
         for k, v in out.items():
@@ -221,9 +245,10 @@ def capture(name, spec, cfg, Network, vr, frames, angle):
                                 chunk_any=np.array(any_all, bool))
             print(f"{path}: {os.path.getsize(path) / 1024:.1f} KiB")
         return
+    wrec = (dict(w_seed=seed, w_gain=gain, w_alpha_bias=ab, w_digest=params_digest(params))
+            if saved is None else {"wt_" + k: v for k, v in params.items()})
     rec = dict(
-        H=spec["H"], W=spec["W"], pose=pose, K=K,
-        w_seed=seed, w_gain=gain, w_alpha_bias=ab, w_digest=params_digest(params),
+        H=spec["H"], W=spec["W"], pose=pose, K=K, **wrec,
         N_samples=cfg.task_arg.N_samples, N_importance=cfg.task_arg.N_importance,
         perturb=float(cfg.task_arg.perturb), lindisp=bool(cfg.task_arg.lindisp),
         enable_ess=bool(rend.enable_ess), enable_ert=bool(rend.enable_ert),

@@ -19,6 +19,8 @@ def load(name):
 
 
 def params_of(z):
+    if "w_seed" not in z:   # stored weights (another topology, the reference's own init)
+        return {k[3:]: z[k] for k in z if k.startswith("wt_")}
     p = make_params(int(z["w_seed"]), float(z["w_gain"]), float(z["w_alpha_bias"]))
     assert params_digest(p) == str(z["w_digest"]), "weight generator drifted from fixture"
     return p
