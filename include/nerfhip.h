@@ -40,8 +40,10 @@ const char* nerf_last_error(void);
  * (2: NerfWgradDesc amax_a2/amax_b2/ldo, NerfX3BwdIO d_raw_t, the
  * nerf_sample_pdf_bwd / nerf_composite_ert arguments of round 4; 3: NerfWgradDesc
  * bsa / bsb, NerfX3TrainOut.bs / NerfX3BwdIO.bs and the encoding-backward layout
- * arguments: the T16 activation layout of round 5) */
-#define NERF_ABI_VERSION 4
+ * arguments: the T16 activation layout of round 5; 4: NerfWgradDesc.a2_row; 5: the
+ * training forward's 65-slice (folded) stream, nerf_fold_views; 6: the backward's
+ * 64-slice (folded) stream, NerfX3BwdIO.d[8] NULL) */
+#define NERF_ABI_VERSION 6
 int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
  * source tree this library was compiled from (nerfhip/_lib.py refuses a
@@ -139,6 +141,20 @@ typedef struct NerfAdamTensor {
 int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float* step,
                    unsigned* done, double beta1, double beta2, float eps, float clip,
                    nerf_stream_t stream);
+/* nerf_fold_views (network.py:63-67): for each of n <= 4 networks, the views
+ *   layer with the feature layer folded in, from the live parameters:
+ *   Wc [128][283] = [W_views[:, :256] W_feat | W_views[:, 256:]] and
+ *   bc [128] = W_views[:, :256] b_feat + b_views (FP32, k ascending) -- the
+ *   views matrix and bias of the training forward's 65-slice stream. */
+typedef struct NerfFoldDesc {
+  const float* Wv;   /* views_linears.0.weight [128][283] */
+  const float* Wf;   /* feature_linear.weight [256][256] */
+  const float* bf;   /* feature_linear.bias [256] */
+  const float* bv;   /* views_linears.0.bias [128] */
+  float* Wc;         /* out [128][283] */
+  float* bc;         /* out [128] */
+} NerfFoldDesc;
+int nerf_fold_views(const NerfFoldDesc* nets, int n, nerf_stream_t stream);
 /* nerf_sum_partials: out[i] = sum_{c=0}^{C-1} part[c * n + i], summed in c
  *   order (the weight-gradient split-K partials of nerf_x3_wgrad). */
 int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_stream_t stream);
@@ -269,23 +285,25 @@ int nerf_x3_wgrad_batch_z(const NerfWgradDesc* descs, int n, const int* tile_chu
                           nerf_stream_t stream);
 
 /* nerf_mlp_train_forward_x3: the whole forward of a training step's MLP in ONE
- *   launch (the inference kernel over the 73-slice stream that keeps the
- *   feature layer: nerfhip.pack.pack_mlp_x3(fold=False), or its device-side
- *   packer nerfhip.train_mlp.X3StreamPacker). Samples p = 0 .. P-1 at pts[p]
+ *   launch (the inference kernel over the 65-slice stream, the feature layer
+ *   folded into the views layer (ABI 5): nerfhip.pack.pack_mlp_x3, or its
+ *   device-side packer nerfhip.train_mlp.X3StreamPacker after nerf_fold_views).
+ *   Samples p = 0 .. P-1 at pts[p]
  *   ([P][3]) with view direction dirs[p]; `zero` = one device float 0.0.
  *   raw[p] = (rgb logits, sigma) as nerf_mlp_forward_x3; besides, every
  *   output is written feature-major with row stride out->ld floats:
- *   act[L] = h_L (rows 0..255) for L = 0..7, act[8] = feature (256 rows),
+ *   act[L] = h_L (rows 0..255) for L = 0..7, act[8]: unused (NULL; the feature
+ *   rows are not computed),
  *   act[9] = the views layer's output (128 rows), act[10] = the xyz encoding
  *   (64 rows: freq.py's 63 columns, row 63 = 0), act[11] = the view encoding
  *   (32 rows: 27 columns, rows 27..31 = 0); bits[L] = the ReLU bits of h_L
  *   (nerf_x3_layer_ex's layout, m_tiles 16) for L = 0..7 and bits[8] those of
  *   the views output (m_tiles 8); amax[0..11] (device floats,
- *   caller-initialised, >= 0) are raised to max |h_0..h_7|, max |feature|,
- *   max |xyz encoding|, max |view encoding|, max |views output|.
- *   act[8] may be NULL: the feature rows are then not written (the weight
- *   gradients can be taken through h_7, nerfhip.train_mlp: dW_views,feat =
- *   G W_feat^T + s b_feat^T with G = d_hv h_7^T). */
+ *   caller-initialised, >= 0) are raised to max |h_0..h_7|, (slot 8 untouched),
+ *   max |xyz encoding|, max |view encoding|, max |views output|. The weight
+ *   gradients of the views and feature layers are taken through h_7
+ *   (nerfhip.train_mlp: dW_views,feat = G W_feat^T + s b_feat^T with
+ *   G = d_hv h_7^T). */
 typedef struct NerfX3TrainOut {
   float* act[12];
   unsigned short* bits[9];
@@ -311,17 +329,18 @@ int nerf_mlp_train_forward_x3_rays(const float* w_slices, const float* w_head,
 
 /* nerf_mlp_train_backward_x3: the backward through the training MLP (the
  *   dgrad chain) in ONE launch, over the transposed-weight stream of
- *   nerfhip.train_mlp.X3BwdStreamPacker (72 slices with_enc, 68 without).
+ *   nerfhip.train_mlp.X3BwdStreamPacker (64 slices with_enc, 60 without; the
+ *   feature layer folded into the views layer as in the forward: its first
+ *   4 slices are Wc[:, :256]^T of nerf_fold_views, ABI 6).
  *   From io->d_raw ([P][4]: d rgb logits, d sigma; 16-byte aligned) and the
  *   forward's ReLU bits (io->bits as NerfX3TrainOut.bits), writes with row
- *   stride io->ld: d[9] = d_hv (128 rows), d[8] = d feature (256), d[7] ..
- *   d[0] = the gradients of the pre-activations of layers 7 .. 0 (256 rows
- *   each); with_enc also d[10] / d[11] = the xyz encoding's gradient through
- *   layer 5 / layer 0 (64 rows; row 63 is padding). io->dmax[0..8], [10]
+ *   stride io->ld: d[9] = d_hv (128 rows), d[7] .. d[0] = the gradients of
+ *   the pre-activations of layers 7 .. 0 (256 rows each); with_enc also
+ *   d[10] / d[11] = the xyz encoding's gradient through layer 5 / layer 0
+ *   (64 rows; row 63 is padding). d[8] must be NULL: d feature does not exist
+ *   (dW_feat = W_views,feat^T G, see NerfX3TrainOut). io->dmax[0..7], [10]
  *   (caller-initialised, >= 0) are raised to the outputs' max |.|, [11] / [12]
- *   to max |d rgb| / |d sigma| of d_raw. d[8] may be
- *   NULL: d feature is then not written (dW_feat = W_views,feat^T G, see
- *   NerfX3TrainOut). */
+ *   to max |d rgb| / |d sigma| of d_raw; [8] is untouched. */
 typedef struct NerfX3BwdIO {
   const float* d_raw;
   const unsigned short* bits[9];
@@ -392,11 +411,13 @@ int nerf_x3_pack(const void* descs, int n, const void* heads, int n_heads, nerf_
 
 /* NET:9-74 for network topologies other than lego's (the fused MLP kernels'
  * one): one nn.Linear (+ ReLU when relu != 0) in FP32 over feature-major
- * activations, Y[m * sym + p * syp] = act(b[m] + sum_k W[m * K + k] X[k * ldx + p])
+ * activations, Y[m * sym + p * syp] = act(b[m] + sum_k W[m * ldw + k] X[k * ldx + p])
  * for m < M, p < P; b nullable; the k sum in ascending order. Used layer by
- * layer by nerfhip.generic_mlp. */
-int nerf_linear_fm(const float* W, const float* b, const float* X, int64_t ldx, int K, int64_t P,
-                   int M, int relu, float* Y, int64_t sym, int64_t syp, nerf_stream_t stream);
+ * layer by nerfhip.generic_mlp, and for the training forward's per-step fold of
+ * the feature layer into the views layer (W_views,feat W_feat). */
+int nerf_linear_fm(const float* W, int64_t ldw, const float* b, const float* X, int64_t ldx,
+                   int K, int64_t P, int M, int relu, float* Y, int64_t sym, int64_t syp,
+                   nerf_stream_t stream);
 
 /* VR:310-314, :1098-1103 (raw_noise_std > 0): out[i] = raw[i] with its density
  * logit (.w) plus noise[i] -- the caller's torch.randn(...) * raw_noise_std in the

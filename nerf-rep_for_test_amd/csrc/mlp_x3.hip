@@ -47,11 +47,11 @@ constexpr int kX3Tile = 16 * kStreamWaves;
 
 // The fragment register sets, live across slices (x: even groups, y: odd),
 // and the stream length (a compile-time constant of each kernel: 65 slices for
-// inference, where the feature layer is folded into the views layer, 73 for
-// the training forward, which keeps it, 72 / 68 for the backward). The
-// backward without the encoding products reads the 72-slice stream minus its
-// encoding slices: logical slice t >= gap is stored at t + 2 (the last two
-// are never reached; nphys slices in memory).
+// inference and the training forward, where the feature layer is folded into
+// the views layer, 64 / 60 for the backward). The backward without the
+// encoding products reads the 64-slice stream minus its encoding slices:
+// logical slice t >= gap is stored at t + 2 (the last two are never reached;
+// nphys slices in memory).
 struct FragPipe {
   Frags x, y;
   int ns;
@@ -558,7 +558,7 @@ __device__ __forceinline__ void mlp_x3_body(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   Ring R{ring, slices, wave, lane};
-  constexpr int kNs = TRAIN ? NERF_MLP_SLICES : kX3Slices;
+  constexpr int kNs = kX3Slices;   // TRAIN too: the feature layer folded (round 5)
 
   for (int t = 0; t < kX3DmaAhead; ++t)   // all 8 waves, 4 pieces each
     stage_slice(TRAIN ? make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane,
@@ -726,24 +726,14 @@ __device__ __forceinline__ void mlp_x3_body(
     }
   }
   // acc holds zeros; X holds h7 (FP32, unsplit)
-  if constexpr (TRAIN) {
-    // ---- the feature layer (NET:63): 256 -> 256, no activation -------------
-    e = act_exponent(sample_max(mx7));
-    s = ldexpf(1.0f, e);
-    split_op(X[0], s);
-    Epi epi{X, ldexpf(1.0f, -((int)hd[kHeadScales + 8] + e)), -__builtin_inff(),
-            lds_addr(hd + kHeadBias + 8 * 256 + g4 * 64), nullptr, 0.0f, 0.0f, true};
-    act_slices(acc, R, g, X, s, fp, epi, st);   // stores h7 pairs 1..7
-    g += 8;
-    amax_to_lds(8, epi.amax);
-    st = store_for(8, 256);                     // the feature rows: the views slices
-    st.template pair<0>(X[0]);
+  if constexpr (TRAIN) {   // h7 pair 1 now; pairs 2..7 ride on the views slices' hooks
     st.template pair<1>(X[1]);
   }
   (void)mx7;
 
-  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67);
-  // inference: feature = W_f h7 + b_f folded in (W_views,feat W_f on h7) ---------
+  // ---- views layer: cat(feature, input_views) 283 -> 128, ReLU (NET:62-67),
+  // feature = W_f h7 + b_f folded in (W_views,feat W_f on h7; training: the
+  // per-step fold of nerf_fold_views) ---------------------------------------------
   Op dirf;
   encode_dir(dv, g4, dirf);
   if constexpr (TRAIN) {   // the view-encoding rows (the views layer's wgrad operand)
@@ -901,27 +891,30 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_train_kernel(
 // inference kernel's per-tile body run through the transposed weights, from
 // the loss gradient d raw [P][4] down to the encoding. Per 128-sample tile:
 //   d_hv = (W_rgb^T d_rgb) * (hv > 0)                 (VALU, FP32; 128 rows)
-//   DF   = W_views[:, :256]^T d_hv                    (4 slices)
-//   D7   = (W_feat^T DF + W_alpha^T d_sigma) * (h7 > 0)    (8 slices)
+//   D7   = (Wc^T d_hv + W_alpha^T d_sigma) * (h7 > 0)  (4 slices)
 //   D_{i-1} = (W_i^T D_i) * (h_{i-1} > 0), i = 7 .. 1 (8 slices each; at i = 5
 //   the h4 rows of W_5, with ENC first d_enc5 = W_5[:, :63]^T D5, 2 slices)
 //   ENC: d_enc0 = W_0^T D0                            (2 slices)
-// (network.py:49-74's autograd; the layer launches of the unfused backward
-// compute the same products). Every output is written feature-major (the weight
+// where Wc = W_views[:, :256] W_feat, the training step's fold of the feature
+// layer (nerf_fold_views; feature = W_feat h7 + b_feat has no activation, so
+// d h7 = W_feat^T W_views,feat^T d_hv + ...: one 128 -> 256 product instead of
+// 128 -> 256 -> 256, and d feature never exists). (network.py:49-74's
+// autograd; the layer launches of the unfused backward compute the same
+// products unfolded.) Every output is written feature-major (the weight
 // gradients read them) and its max |.| raised (their FP16 scales). The ReLU
 // masks are the forward's bits, loaded one slice before the epilogue that
-// applies them. Stream (pack: nerfhip.train_mlp.X3BwdStreamPacker): W_views^T
-// (4), W_feat^T (8), W_7^T, W_6^T (8 each), [W_5,enc^T (2)], W_5,h^T, W_4^T ..
-// W_1^T (8 each), W_0^T (2): 72 slices (without ENC the 4 encoding slices are
-// skipped).
+// applies them. Stream (pack: nerfhip.train_mlp.X3BwdStreamPacker): Wc^T (4),
+// W_7^T, W_6^T (8 each), [W_5,enc^T (2)], W_5,h^T, W_4^T .. W_1^T (8 each),
+// W_0^T (2): 64 slices (without ENC the 4 encoding slices are skipped).
 // ===========================================================================
 constexpr int kBwdScales = 3100;   // per-matrix weight scale exponents [11] in the head
 
 struct X3BwdIO {
   const float4* d_raw;            // [P]: d rgb logits (x, y, z), d sigma (w)
   const unsigned short* bits[9];  // ReLU bits of h0..h7 (m_tiles 16), of the views output (8)
-  float* d[12];                   // 0..7: D0..D7, 8: DF, 9: d_hv, 10: d_enc (layer 5), 11: (layer 0)
-  float* dmax;                    // raised: [i] = max |D_i|, [8] max |DF|, [10] max |d_hv|
+  float* d[12];                   // 0..7: D0..D7, 8: unused (DF: folded), 9: d_hv, 10: d_enc
+                                  // (layer 5), 11: (layer 0)
+  float* dmax;                    // raised: [i] = max |D_i|, [10] max |d_hv| ([8] untouched)
   float* d_raw_t;                 // nullable: rows 0..3 = d sigma, d rgb (x, y, z)
   Lay lay;                        // every output's layout (row stride / T16 block stride)
 };
@@ -1070,17 +1063,17 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   Ring R{ring, slices, wave, lane};
-  constexpr int kNs = ENC ? 72 : 68;
+  constexpr int kNs = ENC ? 64 : 60;
   for (int t = 0; t < kX3DmaAhead; ++t)   // all 8 waves, 4 pieces each
-    stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, 72));
+    stage_slice(make_dma_blocks(slices, t, R.buf(t), wave * kBlocksPerWave, wave, lane, true, 64));
   for (int i = tid; i < kHeadFloats / 4; i += kX3Threads)
     reinterpret_cast<float4*>(hd)[i] = reinterpret_cast<const float4*>(head)[i];
   if (tid < 13) dmax_lds[tid] = 0u;
 
   FragPipe fp;
   fp.ns = kNs;
-  fp.nphys = 72;
-  if (!ENC) fp.gap = 28;   // the encoding slices 28, 29 skipped (70, 71: past the end)
+  fp.nphys = 64;
+  if (!ENC) fp.gap = 20;   // the encoding slices 20, 21 skipped (62, 63: past the end)
   const int64_t ntiles = (P + kX3Tile - 1) / kX3Tile;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const bool first_tile = tile == (int64_t)blockIdx.x;
@@ -1109,7 +1102,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     int ki = k;
     asm volatile("" : "+s"(ki));
     st.rs = rows_rsrc<T16>(io.d[ki], rows, io.lay);
-    st.on = io.d[ki] != nullptr;       // DF may be skipped (d[8] null)
+    st.on = io.d[ki] != nullptr;
     st.rb = __builtin_amdgcn_make_buffer_rsrc((void*)io.d[ki], 0, 0, 0x00020000);
     st.template set_lay<T16>(io.lay, tile, wave);
     st.sboff = 0u;
@@ -1141,6 +1134,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   }
   load_frags<0>(fp.x, lds_base(R.buf(0), lane));
 
+  float mx;   // max |.| of the last product (its FP16 split scale)
   // ---- d_hv = (W_rgb^T d_rgb) * (hv > 0), NET:68-70 backward, FP32 on the VALU
   {
     int i8 = 8;
@@ -1149,7 +1143,7 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     const int64_t wv0 = ((tile * 8 + wave) * 2) * 64 + lane;     // views bits: MT 8
     const unsigned mv0 = bv[wv0], mv1 = bv[wv0 + 64];
     const float* wr = hd + kHeadRgbW + g4 * 32;
-    float mx = 0.0f;
+    mx = 0.0f;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1172,35 +1166,26 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
     const int e = act_exponent(sample_max(mx));
     const float s = ldexpf(1.0f, e);
     split_op(X[4], s);
-    // ---- DF = W_views[:, :256]^T d_hv (4 slices over operands 4..7, so the
-    // epilogue's writes of X[0..6] in the last slice miss its operand; the view
-    // encoding rows are not needed: view directions are constants)
-    BwdEpi<false, false> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + 0] + e)), 0u, 0.0f, 0.0f};
-    { SplitHook h{X[5], s}; slice256x<4, true>(acc, R, 0, X, fp, h); }
-    { SplitHook h{X[6], s}; slice256<5>(acc, R, 1, X, fp, h); }
-    { SplitHook h{X[7], s}; slice256<6>(acc, R, 2, X, fp, h); }
-    slice256<7>(acc, R, 3, X, fp, epi);
-    epi.finish(acc);
-    amax_to_lds(8, epi.amax);
-  }
-  ActStore st = store_for(8, 256);   // DF rows: pair 0 now, 1..7 in the next slices
-  st.template pair<0>(X[0]);
-  int g = 4;
-  float mx = 0.0f;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) mx = fmaxf(mx, op_absmax(X[q]));
-  int e = act_exponent(sample_max(mx));
-  float s = ldexpf(1.0f, e);
-  split_op(X[0], s);
-  {   // ---- D7 = (W_feat^T DF + W_alpha^T d_sigma) * (h7 > 0) (NET:61, 63)
-    BwdEpi<true, true> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + 1] + e)),
+    // ---- D7 = (Wc^T d_hv + W_alpha^T d_sigma) * (h7 > 0) (NET:61, 63-65):
+    // 4 slices over operands 4..7, so the epilogue's writes of X[0..6] in the
+    // last slice miss its operand; the view encoding rows are not needed (view
+    // directions are constants). h7's mask words load in slice 2.
+    BwdEpi<true, true> epi{X, ldexpf(1.0f, -((int)hd[kBwdScales + 0] + e)),
                            lds_addr(hd + kHeadAlphaW + g4 * 64), dr.w, 0.0f, mlane};
     const MaskSrc ms = mask_for(7);
-    dgrad_slices<false>(acc, R, g, X, s, fp, epi, st, ms);
-    g += 8;
+    { SplitHook h{X[5], s}; slice256x<4, true>(acc, R, 0, X, fp, h); }
+    { SplitHook h{X[6], s}; slice256<5>(acc, R, 1, X, fp, h); }
+    { StoreMaskThen<-1, ActStore, SplitHook> h{sv, {X[7], s}, ms, R.wave < 4};
+      slice256<6>(acc, R, 2, X, fp, h); }
+    slice256<7>(acc, R, 3, X, fp, epi);
+    epi.finish(acc);
     amax_to_lds(7, epi.amax);
     mx = epi.amax;
   }
+  int g = 4;
+  ActStore st;
+  int e;
+  float s;
   // ---- D_{i-1} = (W_i^T D_i) * (h_{i-1} > 0), i = 7 .. 1 ---------------------
   for (int i = 7; i >= 1; --i) {
     st = store_for(i, 256);           // D_i rows
@@ -2309,8 +2294,9 @@ extern "C" int nerf_mlp_train_backward_x3(const float* w_slices, const float* w_
   NERF_REQUIRE(w_slices && w_head && io && io->d_raw && io->dmax,
                "nerf_mlp_train_backward_x3: null pointer");
   NERF_REQUIRE(P >= 0 && lay_ok(io->ld, io->bs, P), "nerf_mlp_train_backward_x3: bad layout");
-  for (int i = 0; i < 10; ++i)   // d[8] (DF) may be null: not stored
-    NERF_REQUIRE(i == 8 || io->d[i] != nullptr, "nerf_mlp_train_backward_x3: null output rows");
+  for (int i = 0; i < 10; ++i)   // d[8] (d feature) does not exist: the feature layer is folded
+    NERF_REQUIRE((i == 8) == (io->d[i] == nullptr), "nerf_mlp_train_backward_x3: null output rows"
+                 " (or d[8] set: the folded backward has no d feature)");
   if (with_enc)
     NERF_REQUIRE(io->d[10] && io->d[11], "nerf_mlp_train_backward_x3: null encoding rows");
   for (int i = 0; i < 9; ++i)

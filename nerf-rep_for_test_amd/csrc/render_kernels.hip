@@ -1077,13 +1077,13 @@ int nerf_sample_coarse(const float* z_base, const float* t_rand, int64_t n, int 
 
 // One nn.Linear (+ ReLU) of a NeRF of any topology (NET:9-74), FP32, over
 // feature-major activations: Y[m * sym + p * syp] = act(b[m] + sum_k W[m][k] X[k][p])
-// for m < M, p < P (W row-major [M][K], torch's Linear layout; X [K][ldx]; the
+// for m < M, p < P (W row-major [M][ldw >= K], torch's Linear layout; X [K][ldx]; the
 // output strides write feature-major rows (sym = ldy, syp = 1) or the [P][4]
 // raw record (sym = 1, syp = 4)). The k sum runs in ascending order as one FMA
 // chain per output. The lego topology never comes here (its fused kernels);
 // this is the layer-by-layer path for other D / W / skips / encoding widths.
 // Tile 64 (m) x 64 (p), K steps of 16 through LDS, 4 x 4 outputs per thread.
-__global__ __launch_bounds__(256) void linear_fm_kernel(const float* __restrict__ W,
+__global__ __launch_bounds__(256) void linear_fm_kernel(const float* __restrict__ W, int64_t ldw,
                                                         const float* __restrict__ b,
                                                         const float* __restrict__ X, int64_t ldx,
                                                         int K, int64_t P, int M, int relu,
@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(256) void linear_fm_kernel(const float* __restrict_
       const int e = tid + 256 * r;          // 1024 elements of each tile
       const int wk = e & 15, wm = e >> 4;   // W tile: k fastest (rows of W contiguous)
       const int gm = m0 + wm, gk = k0 + wk;
-      ws[wk][wm] = (gm < M && gk < K) ? W[(int64_t)gm * K + gk] : 0.0f;
+      ws[wk][wm] = (gm < M && gk < K) ? W[(int64_t)gm * ldw + gk] : 0.0f;
       const int xk = e >> 6, xp = e & 63;   // X tile: p fastest
       const int64_t gp = p0 + xp;
       xs[xk][xp] = (k0 + xk < K && gp < P) ? X[(int64_t)(k0 + xk) * ldx + gp] : 0.0f;
@@ -1141,14 +1141,16 @@ __global__ __launch_bounds__(256) void linear_fm_kernel(const float* __restrict_
   }
 }
 
-int nerf_linear_fm(const float* W, const float* b, const float* X, int64_t ldx, int K, int64_t P,
-                   int M, int relu, float* Y, int64_t sym, int64_t syp, nerf_stream_t stream) {
+int nerf_linear_fm(const float* W, int64_t ldw, const float* b, const float* X, int64_t ldx, int K,
+                   int64_t P, int M, int relu, float* Y, int64_t sym, int64_t syp,
+                   nerf_stream_t stream) {
   NERF_REQUIRE(W && X && Y, "nerf_linear_fm: null pointer");
-  NERF_REQUIRE(K >= 1 && M >= 1 && P >= 0 && ldx >= P, "nerf_linear_fm: bad size");
+  NERF_REQUIRE(K >= 1 && M >= 1 && P >= 0 && ldx >= P && ldw >= K, "nerf_linear_fm: bad size");
   NERF_REQUIRE(cdiv(P, 64) < (1ll << 31) && cdiv(M, 64) < 65536, "nerf_linear_fm: too large");
   if (P == 0) return 0;
   hipLaunchKernelGGL(linear_fm_kernel, dim3((unsigned)cdiv(P, 64), (unsigned)cdiv(M, 64)),
-                     dim3(256), 0, as_stream(stream), W, b, X, ldx, K, P, M, relu, Y, sym, syp);
+                     dim3(256), 0, as_stream(stream), W, ldw, b, X, ldx, K, P, M, relu, Y, sym,
+                     syp);
   return check_launch("linear_fm_kernel");
 }
 

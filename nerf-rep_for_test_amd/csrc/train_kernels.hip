@@ -743,4 +743,73 @@ extern "C" int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float*
   return check_launch("adam_kernel");
 }
 
+// The training forward's per-step fold of the feature layer into the views
+// layer (network.py:63-67: feature = W_f h7 + b_f has no activation, so
+// W_v [feat | dir] . cat(feature, d) + b_v = (W_v,feat W_f) h7 + W_v,dir d +
+// (W_v,feat b_f + b_v)): Wc [128][283] = [W_v,feat W_f | W_v,dir] and
+// bc = W_v,feat b_f + b_v from the live parameters, FP32
+// (nerfhip.pack.fold_feature_into_views does the same map in float64 for
+// inference). Block (4 rows, 64 columns, network): wave w sums k in
+// [64 w, 64 w + 64) for column j = its lane (W_f read by row segments,
+// coalesced, all 64 loads in flight), the 4 partial sums added in wave order
+// through LDS; the column-group-0 blocks also take the bias (wave w: row w, a
+// 64-lane split of the sum, then a butterfly) and copy the direction columns.
+constexpr int kFoldMax = 4;
+constexpr int kFoldRows = 4;
+struct FoldBatch {
+  NerfFoldDesc d[kFoldMax];
+};
+
+__global__ __launch_bounds__(256) void fold_views_kernel(const FoldBatch fb) {
+  const NerfFoldDesc& d = fb.d[blockIdx.z];
+  const int m0 = blockIdx.x * kFoldRows, j0 = blockIdx.y * 64, t = threadIdx.x;
+  const int w = t >> 6, lane = t & 63;
+  __shared__ float wrow[kFoldRows][256];
+  __shared__ float part[4][kFoldRows][64];
+#pragma unroll
+  for (int r = 0; r < kFoldRows; ++r) wrow[r][t] = d.Wv[(m0 + r) * 283 + t];
+  float wf[64];
+#pragma unroll
+  for (int k = 0; k < 64; ++k) wf[k] = d.Wf[(64 * w + k) * 256 + j0 + lane];
+  __syncthreads();
+  float acc[kFoldRows] = {};
+#pragma unroll
+  for (int k = 0; k < 64; ++k)
+#pragma unroll
+    for (int r = 0; r < kFoldRows; ++r) acc[r] = __builtin_fmaf(wrow[r][64 * w + k], wf[k], acc[r]);
+#pragma unroll
+  for (int r = 0; r < kFoldRows; ++r) part[w][r][lane] = acc[r];
+  __syncthreads();
+  {
+    const int r = w;   // wave w writes row m0 + w
+    const float v = ((part[0][r][lane] + part[1][r][lane]) + part[2][r][lane]) + part[3][r][lane];
+    d.Wc[(m0 + r) * 283 + j0 + lane] = v;
+  }
+  if (blockIdx.y != 0) return;
+  if (t < 27) {
+#pragma unroll
+    for (int r = 0; r < kFoldRows; ++r)
+      d.Wc[(m0 + r) * 283 + 256 + t] = d.Wv[(m0 + r) * 283 + 256 + t];
+  }
+  float b = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b = __builtin_fmaf(wrow[w][lane * 4 + q], d.bf[lane * 4 + q], b);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) b += __shfl_xor(b, o);
+  if (lane == 0) d.bc[m0 + w] = b + d.bv[m0 + w];
+}
+
+extern "C" int nerf_fold_views(const NerfFoldDesc* nets, int n, nerf_stream_t stream) {
+  NERF_REQUIRE(nets && n >= 1 && n <= kFoldMax, "nerf_fold_views: bad arguments");
+  FoldBatch fb;
+  for (int k = 0; k < n; ++k) {
+    const NerfFoldDesc& d = nets[k];
+    NERF_REQUIRE(d.Wv && d.Wf && d.bf && d.bv && d.Wc && d.bc, "nerf_fold_views: null pointer");
+    fb.d[k] = d;
+  }
+  hipLaunchKernelGGL(fold_views_kernel, dim3(128 / kFoldRows, 4, (unsigned)n), dim3(256), 0, as_stream(stream),
+                     fb);
+  return check_launch("fold_views_kernel");
+}
+
 }  // namespace nerfhip

@@ -10,7 +10,7 @@ import os
 import threading
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ABI_VERSION = 4   # include/nerfhip.h NERF_ABI_VERSION
+ABI_VERSION = 6   # include/nerfhip.h NERF_ABI_VERSION
 LIB_PATH = os.environ.get("NERFHIP_LIB", os.path.join(PKG_ROOT, "lib", "libnerfhip.so"))
 
 MLP_SLICES = 73
@@ -60,7 +60,8 @@ SIGNATURES = {
                                              _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_add_sigma_noise": (_I, [_P, _P, _I64, _P, _S]),
-    "nerf_linear_fm": (_I, [_P, _P, _P, _I64, _I, _I64, _I, _I, _P, _I64, _I64, _S]),
+    "nerf_fold_views": (_I, [_P, _I, _S]),
+    "nerf_linear_fm": (_I, [_P, _I64, _P, _P, _I64, _I, _I64, _I, _I, _P, _I64, _I64, _S]),
     "nerf_composite_ert_workspace": (_SZ, [_I64, _I]),
     "nerf_composite_ert": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _F, _I, _P, _P, _P, _P, _P, _P,
                                 _S]),

@@ -58,7 +58,7 @@ class GenericMLP:
     def _lin(self, wb, X, ldx, K, P, relu, Y, sym, syp, st):
         w, b = wb
         assert tuple(w.shape)[1] == K
-        call("nerf_linear_fm", ptr(w), ptr(b), ptr(X), ldx, K, P, int(w.shape[0]), int(relu),
+        call("nerf_linear_fm", ptr(w), K, ptr(b), ptr(X), ldx, K, P, int(w.shape[0]), int(relu),
              ptr(Y), sym, syp, st)
 
     def forward(self, rays_o, rays_d, z, z_stride, n, S):

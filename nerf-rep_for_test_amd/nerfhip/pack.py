@@ -332,23 +332,29 @@ def fold_feature_into_views(Wf, bf, Wv, bv):
     return W.astype(np.float32), b.astype(np.float32)
 
 
-def pack_mlp_x3(params, prefix="model", fold=True):
-    """Packed network for nerf_mlp_forward_x3: (slices float32[65*8192] holding
-    FP16 fragment pairs, head float32[3200]). The feature layer is folded into
-    the views layer (fold_feature_into_views): 11 % fewer MACs per sample.
-    fold=False: the 73-slice stream of nerf_mlp_train_forward_x3, which keeps
-    the feature layer (8 slices between layer 7 and the views layer; the head
-    then carries the feature bias and the unfolded views bias)."""
+def pack_mlp_x3(params, prefix="model", fold=True, folded=None):
+    """Packed network for nerf_mlp_forward_x3 and nerf_mlp_train_forward_x3:
+    (slices float32[65*8192] holding FP16 fragment pairs, head float32[3200]).
+    The feature layer is folded into the views layer (fold_feature_into_views,
+    float64): 11 % fewer MACs per sample. folded=(Wc [128, 283], bc [128]): that
+    fold given (the training forward's per-step FP32 fold, nerf_fold_views).
+    fold=False: the 73-slice stream that keeps the feature layer (8 slices
+    between layer 7 and the views layer; the head then carries the feature
+    bias and the unfolded views bias; the layer-launch path's reference)."""
     def get(name):
         v = params[f"{prefix}.{name}"]
         v = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
         return np.ascontiguousarray(v, np.float32)
 
     _, head = pack_mlp(params, prefix)          # biases and VALU heads: same layout
-    if fold:
+    if fold and folded is not None:
+        Wc, bc = (np.ascontiguousarray(np.asarray(a.detach().cpu() if hasattr(a, "detach") else a),
+                                       np.float32) for a in folded)
+    elif fold:
         Wc, bc = fold_feature_into_views(get("feature_linear.weight"), get("feature_linear.bias"),
                                          get("views_linears.0.weight"),
                                          get("views_linears.0.bias"))
+    if fold:
         head[H_BIAS_VIEWS:H_BIAS_VIEWS + 128] = _group_pack(bc, 8).reshape(-1)
         head[H_BIAS + 8 * 256:H_BIAS + 9 * 256] = 0.0   # feature bias: folded
     slices = []

@@ -202,41 +202,64 @@ def _src_pointers(p, names, idx, amax, nsrc):
     return out
 
 
+class NerfFoldDescC(ctypes.Structure):
+    """NerfFoldDesc (include/nerfhip.h)."""
+    _fields_ = [(k, ctypes.c_void_p) for k in ("Wv", "Wf", "bf", "bv", "Wc", "bc")]
+
+
+def _fold(packers):
+    """One nerf_fold_views launch for the forward streams of several networks."""
+    arr = (NerfFoldDescC * len(packers))(*[NerfFoldDescC(*f.fold_ptrs) for f in packers])
+    call("nerf_fold_views", ctypes.addressof(arr), len(packers), _lib.stream_of(packers[0].device))
+
+
 class X3StreamPacker(_PackSet):
     """The training forward's weight stream, packed on the device from the live
-    parameters: the 73 slices of nerf_mlp_train_forward_x3 (the inference
-    kernel's layout with the feature layer kept: byte-identical to
-    nerfhip.pack.pack_mlp_x3(fold=False)), each layer's matrix with the kernel's
-    K permutation as its column map, written straight into its slices, and the
-    head block (lane-packed biases, the alpha / rgb heads, the per-layer weight
-    scales) gathered from the parameters through an index map made once by
-    nerfhip.pack.pack_mlp -- all in the nerf_x3_pack launch set."""
+    parameters: the 65 slices of nerf_mlp_train_forward_x3 -- the inference
+    kernel's layout, the feature layer folded into the views layer each step
+    by nerf_fold_views into (Wc, bc) (byte-identical to
+    nerfhip.pack.pack_mlp_x3(params, folded=(Wc, bc))), each layer's matrix with
+    the kernel's K permutation as its column map, written straight into its
+    slices, and the head block (lane-packed biases, the alpha / rgb heads, the
+    per-layer weight scales) gathered from the parameters (the views bias from
+    bc) through an index map made once by nerfhip.pack.pack_mlp -- all in the
+    nerf_x3_pack launch set, after the fold."""
 
     @staticmethod
     def plan():
         from .pack import _x3_layer_cols, layer_plan
         out, off = [], 0
-        for name, kind, tiles in layer_plan():
+        for li, (name, kind, tiles) in enumerate(layer_plan()):
+            if name == "feature_linear":   # folded into the views layer
+                continue
             cols = _x3_layer_cols(kind).reshape(-1)
-            out.append((name + ".weight", list(range(16 * tiles)), [int(c) for c in cols], off))
+            out.append((name + ".weight", list(range(16 * tiles)), [int(c) for c in cols], off, li))
             off += -(-16 * tiles * len(cols) // 8192)          # whole slices (views: 4.5 -> 5)
         return out, off
 
     def _build(self, p):
         import numpy as np
-        from .pack import HEAD_FLOATS, H_SCALES, SLICE_FLOATS, pack_mlp
+        from .pack import H_BIAS, HEAD_FLOATS, H_SCALES, SLICE_FLOATS, pack_mlp
         dev = self.device
         plan, nsl = self.plan()
         self.recs, self.heads, self._keep, self._tables = [], [], [], (None, None)
         self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
         self.sw = torch.zeros(len(plan), device=dev, dtype=torch.int32)
         self.amax = torch.zeros(len(plan), device=dev, dtype=torch.int32)
-        for n, (pname, rmap, cmap, off) in enumerate(plan):
-            self._matrix(p[pname], rmap, cmap, False,
+        self.Wc = torch.zeros((128, 283), device=dev, dtype=torch.float32)
+        self.bc = torch.zeros((128,), device=dev, dtype=torch.float32)
+        src = [p[k] for k in ("views_linears.0.weight", "feature_linear.weight",
+                              "feature_linear.bias", "views_linears.0.bias")]
+        assert all(t.is_contiguous() for t in src)
+        self.fold_ptrs = tuple(t.data_ptr() for t in src) + (self.Wc.data_ptr(), self.bc.data_ptr())
+        for n, (pname, rmap, cmap, off, _) in enumerate(plan):
+            W = self.Wc if pname == "views_linears.0.weight" else p[pname]
+            self._matrix(W, rmap, cmap, False,
                          self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
                          self.sw[n:n + 1].data_ptr(), self.amax[n:n + 1].data_ptr())
         # head: which source element every head float is (pack_mlp on index-valued
-        # parameters); sources = HEAD_SRC parameters flattened, then the 10 scales
+        # parameters); sources = HEAD_SRC parameters flattened (the views bias: bc),
+        # then the 9 scales
         src_n = [sum(int(np.prod(p[k].shape)) for k in HEAD_SRC[:i]) for i in range(len(HEAD_SRC))]
         fake = {}
         for k, v in PARAM_SHAPES.items():
@@ -247,10 +270,15 @@ class X3StreamPacker(_PackSet):
         _, head = pack_mlp(fake, "model")
         nsrc = src_n[-1] + int(np.prod(p[HEAD_SRC[-1]].shape))
         idx = np.rint(head).astype(np.int64) - 1              # -1: zero
-        idx[H_SCALES:H_SCALES + len(plan)] = nsrc + np.arange(len(plan))
+        idx[H_BIAS + 8 * 256:H_BIAS + 9 * 256] = -1             # the feature bias: folded
+        idx[H_SCALES:H_SCALES + 10] = -1                        # the feature layer's scale: 0
+        for n, (_, _, _, _, li) in enumerate(plan):
+            idx[H_SCALES + li] = nsrc + n
         assert idx.max() < nsrc + len(plan) and head.shape[0] == HEAD_FLOATS
         self.head = torch.zeros(HEAD_FLOATS, device=dev, dtype=torch.float32)
-        self._head(_src_pointers(p, HEAD_SRC, idx, self.amax, nsrc), self.head)
+        pp = dict(p)
+        pp["views_linears.0.bias"] = self.bc
+        self._head(_src_pointers(pp, HEAD_SRC, idx, self.amax, nsrc), self.head)
 
     def pack(self, p):
         """p: parameter name (PARAM_NAMES) -> tensor. Returns (stream, head) on the device."""
@@ -258,6 +286,7 @@ class X3StreamPacker(_PackSet):
         if key != self.key:
             self._build(p)
             self.key = key
+        _fold([self])
         self.launch()
         return self.stream, self.head
 
@@ -266,12 +295,16 @@ class X3BwdStreamPacker(_PackSet):
     """The backward chain's weight stream (nerf_mlp_train_backward_x3), packed on
     the device: the transposed matrices in consumption order, each with the
     register-resident K permutation (x3_cols_act) as its column map --
-    W_views[:, :256]^T (4 slices), W_feat^T, W_7^T, W_6^T (8 each), the
-    encoding rows of W_5^T (2 slices of 4 tiles x 4 K steps), the h4 rows of
-    W_5^T, W_4^T .. W_1^T (8 each), W_0^T (2 slices): 72 slices (the kernel
-    without the encoding products skips slices 28, 29, 70, 71) -- and its head:
-    the lane-packed rgb and alpha weights at the forward head's offsets, the 11
-    weight scales at 3100 + j (j = matrix in that order)."""
+    Wc[:, :256]^T (4 slices; Wc = the fold of the feature layer into the views
+    layer, nerf_fold_views, so d h7 comes out of one 128 -> 256 product),
+    W_7^T, W_6^T (8 each), the encoding rows of W_5^T (2 slices of 4 tiles x 4
+    K steps), the h4 rows of W_5^T, W_4^T .. W_1^T (8 each), W_0^T (2 slices):
+    64 slices (the kernel without the encoding products skips slices 20, 21,
+    62, 63) -- and its head: the lane-packed rgb and alpha weights at the
+    forward head's offsets, the weight scales at 3100 + j (j: Wc 0, W_7 2,
+    W_6 3, W_5,enc 4, W_5,h 5, W_4 .. W_1 6 .. 9, W_0 10; slot 1, the unfolded
+    feature layer's, stays 0). Wc: the forward packer's fold of the same
+    parameters (X3NetPacker), or None: this packer folds them itself."""
 
     @staticmethod
     def plan():
@@ -280,30 +313,37 @@ class X3BwdStreamPacker(_PackSet):
         act = [int(c) for c in x3_cols_act().reshape(-1)]
         act4 = [int(c) for c in x3_cols_act(4).reshape(-1)]
         enc = ar(63) + [-1]
-        mats = [("views_linears.0.weight", ar(256), act4), ("feature_linear.weight", ar(256), act),
-                ("pts_linears.7.weight", ar(256), act), ("pts_linears.6.weight", ar(256), act),
-                ("pts_linears.5.weight", enc, act),
-                ("pts_linears.5.weight", [63 + i for i in range(256)], act)]
-        mats += [(f"pts_linears.{i}.weight", ar(256), act) for i in (4, 3, 2, 1)]
-        mats += [("pts_linears.0.weight", enc, act)]
+        mats = [("fold", ar(256), act4, 0), ("pts_linears.7.weight", ar(256), act, 2),
+                ("pts_linears.6.weight", ar(256), act, 3), ("pts_linears.5.weight", enc, act, 4),
+                ("pts_linears.5.weight", [63 + i for i in range(256)], act, 5)]
+        mats += [(f"pts_linears.{i}.weight", ar(256), act, 10 - i) for i in (4, 3, 2, 1)]
+        mats += [("pts_linears.0.weight", enc, act, 10)]
         out, off = [], 0
-        for j, (name, rmap, cmap) in enumerate(mats):
+        for name, rmap, cmap, j in mats:
             out.append((name, rmap, cmap, off, j))
             off += -(-len(rmap) * len(cmap) // 8192)
         return out, off
 
-    def _build(self, p):
+    def _build(self, p, Wc=None):
         import numpy as np
         from .pack import H_ALPHA_W, H_RGB_W, HEAD_FLOATS, SLICE_FLOATS, _group_pack
         dev = self.device
         plan, nsl = self.plan()
         self.recs, self.heads, self._keep, self._tables = [], [], [], (None, None)
+        self.own_fold = Wc is None
+        if Wc is None:   # standalone: its own fold of the parameters
+            Wc = self.Wc = torch.zeros((128, 283), device=dev, dtype=torch.float32)
+            self.bc = torch.zeros((128,), device=dev, dtype=torch.float32)
+            self.fold_ptrs = tuple(p[k].data_ptr() for k in (
+                "views_linears.0.weight", "feature_linear.weight", "feature_linear.bias",
+                "views_linears.0.bias")) + (self.Wc.data_ptr(), self.bc.data_ptr())
         self.stream = torch.zeros(nsl * SLICE_FLOATS, device=dev, dtype=torch.float32)
         self.sw = torch.zeros(11, device=dev, dtype=torch.int32)
         self.amax = torch.zeros(11, device=dev, dtype=torch.int32)
         for name, rmap, cmap, off, j in plan:
             # transposed: element (i, k) = W[cmap[k]][rmap[i]]
-            self._matrix(p[name], rmap, cmap, True, self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
+            self._matrix(Wc if name == "fold" else p[name], rmap, cmap, True,
+                         self.stream.data_ptr() + 4 * off * SLICE_FLOATS,
                          self.sw[j:j + 1].data_ptr(), self.amax[j:j + 1].data_ptr())
         # head: rgb W [3][4][32] and alpha W [4][64] lane-packed (pack_mlp's layout),
         # then the scales: sources = cat(rgb W (384), alpha W (256)), scales
@@ -322,6 +362,7 @@ class X3BwdStreamPacker(_PackSet):
         if key != self.key:
             self._build(p)
             self.key = key
+        _fold([self])
         self.launch()
         return self.stream, self.head
 
@@ -345,7 +386,7 @@ class X3NetPacker:
         key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
         if key != self.key:
             self.fwd._build(p)
-            self.bwd._build(p)
+            self.bwd._build(p, self.fwd.Wc)   # Wc^T: the forward's fold, made first
             self.fwd.key = self.bwd.key = self.key = key
             self.pending = False
 
@@ -385,6 +426,7 @@ def _launch_packs(nets):
         tabs = _PACK_TABLES[key] = (_device_table(recs, _DESC_FIELDS, dev), len(recs),
                                     _device_table(heads, _HEAD_FIELDS, dev), len(heads))
     descs, n, htab, nh = tabs
+    _fold([net.fwd for net in nets])   # the views matrices the packs read
     call("nerf_x3_pack", ptr(descs), n, ptr(htab), nh, _lib.stream_of(nets[0].device))
 
 
@@ -873,7 +915,11 @@ class NerfMLPFn(torch.autograd.Function):
         stats = torch.zeros(25, device=dev, dtype=f32)   # amax + the backward's dmax: one fill
         amax, ctx.dmax_buf = stats[:12], stats[12:]
         pts_c = pts.detach().contiguous()
-        fused_f, fused_b = FUSED_FORWARD and P > 0, FUSED_BACKWARD and P > 0
+        # the fused backward reads the fused forward's rows (V = [h7; view enc]:
+        # with the feature layer folded there is no d feature for the layer
+        # launches' feature-row weight gradient): it follows the fused forward
+        fused_f = FUSED_FORWARD and P > 0
+        fused_b = FUSED_BACKWARD and fused_f
         if fused_f and fused_b and _t16_ok(P):
             ctx.fused_backward = True
             ctx.streams = _streams_for(params, dev)
@@ -1040,7 +1086,7 @@ class NerfMLPFn(torch.autograd.Function):
         need_enc = ctx.pts_grad and ctx.needs_input_grad[2 if rays_S else 0]
         if ctx.fused_backward:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_fused(
-                d_raw_c, ctx.streams[2:], bits, bits_v, dmax, need_enc, not v_h7,
+                d_raw_c, ctx.streams[2:], bits, bits_v, dmax, need_enc,
                 HX if heads_merged else None, bbuf)
         else:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
@@ -1175,15 +1221,15 @@ def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):
     return d_hv, DF, D, d_enc
 
 
-def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=True, hx=None,
-                         bbuf=None):
+def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, hx=None, bbuf=None):
     """The same chain as ONE nerf_mlp_train_backward_x3 launch over the
-    transposed weight stream (X3BwdStreamPacker): every product's rows written
-    feature-major and its max |.| raised, the ReLU masks from the forward's
-    bits; d_enc = the layer-5 and layer-0 encoding rows. store_df=False: DF is
-    not written (None; the weight gradients go through G, NerfMLPFn.backward).
-    hx: a [132, P] row buffer: d_hv goes to rows 0..127 and d raw, feature-major,
-    to rows 128..131 (d sigma, d r, d g, d b)."""
+    transposed weight stream (X3BwdStreamPacker, the feature layer folded into
+    the views layer): every product's rows written feature-major and its max
+    |.| raised, the ReLU masks from the forward's bits; d_enc = the layer-5 and
+    layer-0 encoding rows. DF (d feature) does not exist: None (the views and
+    feature weight gradients go through G, NerfMLPFn.backward). hx: a [132, P]
+    row buffer: d_hv goes to rows 0..127 and d raw, feature-major, to rows
+    128..131 (d sigma, d r, d g, d b)."""
     dev = d_raw.device
     P = d_raw.shape[0]
     stream, head = streams
@@ -1191,15 +1237,13 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=
     if d_raw_c.data_ptr() % 16:
         d_raw_c = d_raw_c.clone()
     if bbuf is not None:   # T16: every row in the one buffer (_BWD_*), hx its first rows
-        assert hx is not None and not store_df
+        assert hx is not None
         D = [bbuf.rows(_BWD_D + 256 * i, _BWD_D + 256 * (i + 1)) for i in range(8)]
-        DF = None
         d_hv = hx.rows(0, 128)
         de5 = bbuf.rows(_BWD_E5, _BWD_E5 + 64) if need_enc else None
         de0 = bbuf.rows(_BWD_E0, _BWD_E0 + 64) if need_enc else None
     else:
         D = [_act(256, P, dev) for _ in range(8)]
-        DF = _act(256, P, dev) if store_df else None
         d_hv = _act(128, P, dev) if hx is None else hx[0:128]
         de5 = _act(64, P, dev) if need_enc else None
         de0 = _act(64, P, dev) if need_enc else None
@@ -1209,7 +1253,7 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=
         io.bits[i] = bits[i].data_ptr()
         io.d[i] = D[i].data_ptr()
     io.bits[8] = bits_v.data_ptr()
-    io.d[8], io.d[9] = (DF.data_ptr() if store_df else None), d_hv.data_ptr()
+    io.d[8], io.d[9] = None, d_hv.data_ptr()
     io.d[10] = de5.data_ptr() if need_enc else None
     io.d[11] = de0.data_ptr() if need_enc else None
     io.dmax = dmax.data_ptr()
@@ -1219,12 +1263,11 @@ def _backward_fused_impl(d_raw, streams, bits, bits_v, dmax, need_enc, store_df=
     else:
         io.ld, io.bs = D[0].stride(0), 0
         io.d_raw_t = hx[128].data_ptr() if hx is not None else None
-        assert all(t.stride(0) == io.ld for t in [d_hv] + ([DF] if store_df else []) +
-                   ([de5, de0] if need_enc else []))
+        assert all(t.stride(0) == io.ld for t in [d_hv] + ([de5, de0] if need_enc else []))
     call("nerf_mlp_train_backward_x3", ptr(stream), ptr(head), P, int(bool(need_enc)),
          ctypes.addressof(io), _lib.stream_of(dev))
     d_enc = (rows_of(de5, 0, 63), rows_of(de0, 0, 63)) if need_enc else None
-    return d_hv, DF, D, d_enc
+    return d_hv, None, D, d_enc
 
 
 NerfMLPFn._backward_layers = staticmethod(_backward_layers_impl)

@@ -40,13 +40,13 @@ def test_linear_fm_matches_float64(dev, M, K, P, relu):
     if relu:
         ref = ref.clamp_min(0)
     Y = torch.full((M, P), float("nan"), device=dev)
-    call("nerf_linear_fm", ptr(W), ptr(b), ptr(X), P + 3, K, P, M, relu, ptr(Y), P, 1,
+    call("nerf_linear_fm", ptr(W), K, ptr(b), ptr(X), P + 3, K, P, M, relu, ptr(Y), P, 1,
          stream_of(dev))
     scale = (W.double().abs() @ X[:, :P].double().abs()).max(1).values + 1.0
     assert float(((Y.double() - ref).abs().max(1).values / scale).max()) < 1e-6
     if M <= 4:   # the raw record: Y[m + 4 p]
         R = torch.full((P, 4), float("nan"), device=dev)
-        call("nerf_linear_fm", ptr(W), ptr(b), ptr(X), P + 3, K, P, M, relu, ptr(R), 1, 4,
+        call("nerf_linear_fm", ptr(W), K, ptr(b), ptr(X), P + 3, K, P, M, relu, ptr(R), 1, 4,
              stream_of(dev))
         assert torch.equal(R[:, :M].t().contiguous(), Y)
 

@@ -444,37 +444,60 @@ def test_x3_wgrad_batch_joined_column_blocks(dev):
 
 
 def test_x3_stream_packer_matches_host_packing(dev):
-    """X3StreamPacker (nerf_x3_pack into the 73-slice stream + the head gather)
-    == nerfhip.pack.pack_mlp_x3(fold=False): the stream bit for bit, the head
-    value for value (scales included)."""
+    """X3StreamPacker (nerf_fold_views, then nerf_x3_pack into the 65-slice
+    stream + the head gather) == nerfhip.pack.pack_mlp_x3 given the same fold:
+    the stream bit for bit, the head value for value (scales included); the
+    device fold (FP32) within 1e-6 of the float64 fold of
+    fold_feature_into_views, relative to each row's magnitude."""
+    import numpy as np
     from nerfhip.pack import pack_mlp_x3
     from nerfhip.train_mlp import PARAM_NAMES, X3StreamPacker, mlp_params
     m = _model(dev, seed=3, gain=2.5)
     p = dict(zip(PARAM_NAMES, mlp_params(m)))
-    stream, head = X3StreamPacker(dev).pack(p)
-    ref_s, ref_h = pack_mlp_x3({"model." + k: v.detach().cpu() for k, v in p.items()}, fold=False)
+    pk = X3StreamPacker(dev)
+    stream, head = pk.pack(p)
+    hp = {"model." + k: v.detach().cpu() for k, v in p.items()}
+    ref_s, ref_h = pack_mlp_x3(hp, folded=(pk.Wc, pk.bc))
+    assert stream.numel() == 65 * 8192
     assert torch.equal(stream.view(torch.int32).cpu(), torch.from_numpy(ref_s).view(torch.int32))
     assert torch.equal(head.cpu(), torch.from_numpy(ref_h))
+    g = lambda k: hp["model." + k].numpy().astype(np.float64)   # noqa: E731
+    Wf, bf, Wv, bv = (g(k) for k in ("feature_linear.weight", "feature_linear.bias",
+                                     "views_linears.0.weight", "views_linears.0.bias"))
+    W64 = np.concatenate([Wv[:, :256] @ Wf, Wv[:, 256:]], 1)
+    b64 = Wv[:, :256] @ bf + bv
+    scale = np.abs(Wv[:, :256]) @ np.abs(Wf)
+    assert np.max(np.abs(pk.Wc.cpu().numpy()[:, :256] - W64[:, :256]) / (scale + 1e-30)) < 1e-6
+    assert np.array_equal(pk.Wc.cpu().numpy()[:, 256:], Wv[:, 256:].astype(np.float32))
+    sb = np.abs(Wv[:, :256]) @ np.abs(bf) + np.abs(bv)
+    assert np.max(np.abs(pk.bc.cpu().numpy() - b64) / (sb + 1e-30)) < 1e-6
+
 
 
 def test_x3_bwd_stream_packer_matches_host_packing(dev):
     """X3BwdStreamPacker: every transposed matrix's slices == pack_x3_matrix of
     that matrix (rows / K columns through the plan's maps, -1 -> 0) bit for bit,
-    at the slice offsets the backward kernel consumes (72 slices); the
-    head's rgb / alpha weights where the forward head holds them, the scales at
-    3100 + matrix index."""
+    at the slice offsets the backward kernel consumes (64 slices; the first
+    four: the fold Wc[:, :256]^T, which equals the forward packer's fold bit for
+    bit); the head's rgb / alpha weights where the forward head holds them, the
+    scales at 3100 + matrix slot (slot 1, the unfolded feature layer's: 0)."""
     import numpy as np
     from nerfhip.pack import H_ALPHA_W, H_RGB_W, SLICE_FLOATS, pack_mlp
-    from nerfhip.train_mlp import PARAM_NAMES, X3BwdStreamPacker, mlp_params, pack_x3_matrix
+    from nerfhip.train_mlp import (PARAM_NAMES, X3BwdStreamPacker, X3StreamPacker, mlp_params,
+                                   pack_x3_matrix)
     m = _model(dev, seed=3, gain=2.5)
     p = dict(zip(PARAM_NAMES, mlp_params(m)))
     pk = X3BwdStreamPacker(dev)
     stream, head = pk.pack(p)
     plan, nsl = pk.plan()
-    assert nsl == 72 and stream.numel() == nsl * SLICE_FLOATS
+    assert nsl == 64 and stream.numel() == nsl * SLICE_FLOATS
+    fwd = X3StreamPacker(dev)
+    fwd.pack(p)
+    assert torch.equal(pk.Wc.view(torch.int32), fwd.Wc.view(torch.int32))
     hd = head.cpu()
+    assert int(hd[3101]) == 0
     for name, rmap, cmap, off, j in plan:
-        Wt = p[name].detach().t()
+        Wt = (pk.Wc if name == "fold" else p[name]).detach().t()
         rm, cm = torch.tensor(rmap, device=dev), torch.tensor(cmap, device=dev)
         T = torch.where((rm >= 0)[:, None] & (cm >= 0)[None, :],
                         Wt[rm.clamp_min(0)][:, cm.clamp_min(0)], 0.0)   # +0.0, as the kernel
@@ -520,6 +543,9 @@ def test_fused_train_forward_equals_layer_launches(dev, P, monkeypatch):
         assert a.shape == b.shape, name
         if name == "V":
             a, b = a[256:], b[256:]
+        if name == "amax":   # slot 8 (feature rows): the fused forward folds that layer away
+            assert float(a[8]) == 0.0
+            a, b = torch.cat([a[:8], a[9:]]), torch.cat([b[:8], b[9:]])
         assert _rel(a, b) < 1e-6, (name, _rel(a, b))
     assert torch.equal(s1[9][:256], s1[8])              # fused: V[:256] is h7
     # ReLU bits (x3_layer_kernel's word layout, what the dgrad launches read):
@@ -558,11 +584,13 @@ def _dense(t):
 @pytest.mark.parametrize("P", [1, 130, 4096, 70001])
 def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatch):
     """nerf_mlp_train_backward_x3 (one launch) against the layer launches it
-    replaces, after the same forward: d hv, DF, D0..D7 and the encoding
-    gradient rows within 1e-5 of each tensor's max (d hv: FP32 on the VALU
-    instead of an x3 product over the 3 rgb rows; the rest the same x3
-    products), every max |.| slot within 1e-5, the same zeros (the forward's
-    ReLU bits), and the parameter / point gradients within 1e-5."""
+    replaces, after the same forward: d hv, D0..D7 and the encoding gradient
+    rows within 1e-5 of each tensor's max (d hv: FP32 on the VALU instead of an
+    x3 product over the 3 rgb rows; D7 through the fold Wc = W_views,feat
+    W_feat in one product instead of two; the rest the same x3 products), every
+    max |.| slot within 1e-5 (but DF's: the fused kernel has no d feature), the
+    same zeros (the forward's ReLU bits), and the parameter / point gradients
+    within 1e-5."""
     from nerfhip import train_mlp
     from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
     m = _model(dev, seed=7, gain=2.0)
@@ -601,7 +629,9 @@ def test_fused_train_backward_equals_layer_launches(dev, P, pts_grad, monkeypatc
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
         if name not in ("DF", "d_enc5", "d_enc0"):   # masked products: the same zeros
             assert float(((a == 0) != (b == 0)).float().mean()) <= 1e-6, name
-    assert torch.allclose(m1, m0, rtol=1e-5, atol=0), (m1, m0)   # (slot 8: DF's max, both)
+    assert float(m1[8]) == 0.0 and float(m0[8]) > 0.0          # slot 8: DF's max (layers only)
+    keep = [i for i in range(m0.numel()) if i != 8]
+    assert torch.allclose(m1[keep], m0[keep], rtol=1e-5, atol=0), (m1, m0)
     for name, a, b in zip((["pts"] if pts_grad else []) + PARAM_NAMES, grads[True], grads[False]):
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
 

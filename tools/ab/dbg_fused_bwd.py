@@ -35,7 +35,7 @@ def main(P=1000):
             out = fn(*a)
             torch.cuda.synchronize()
             rows = [out[0], out[1], *out[2]] + (list(out[3]) if out[3] is not None else [])
-            rec[key] = ([t.clone() for t in rows], a[di].clone())
+            rec[key] = ([None if t is None else t.clone() for t in rows], a[di].clone())
             return out
         setattr(NerfMLPFn, attr, staticmethod(w))
     grads = {}
@@ -47,6 +47,8 @@ def main(P=1000):
         torch.cuda.synchronize()
     names = ["d_hv", "DF"] + [f"D{i}" for i in range(8)] + ["d_enc5", "d_enc0"]
     for name, a, b in zip(names, rec[True][0], rec[False][0]):
+        if a is None:   # DF: the fused kernel folds the feature layer away
+            continue
         e = (a - b).abs()
         rel = float(e.max() / b.abs().max().clamp_min(1e-30))
         bad = torch.isnan(a).sum().item()
