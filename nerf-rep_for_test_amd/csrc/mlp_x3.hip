@@ -1362,15 +1362,12 @@ __device__ __forceinline__ void vm_wait_n(int n) {   // s_waitcnt vmcnt(n), n un
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
@@ -1782,15 +1779,6 @@ constexpr int kWgRing = 5;
 #ifndef NERF_WGRAD_ABL
 #define NERF_WGRAD_ABL 0
 #endif
-// NERF_WGRAD_PF = D > 0 (study): every wave also loads one dword per 128-B line
-// of its operand's K step k + D at the start of step k (A: waves 0-3, B: 4-7),
-// so the step's LDS-DMA, issued at step k + D - 2, finds it in L2
-#ifndef NERF_WGRAD_PF
-#define NERF_WGRAD_PF 0
-#endif
-#ifndef NERF_WGRAD_LIN
-#define NERF_WGRAD_LIN 0
-#endif
 __device__ __forceinline__ void wgrad_dma_body(
     uint4 (&ring)[kWgRing][32 * 64], const float* __restrict__ A, int64_t lda, int M,
     const float* __restrict__ B, int64_t ldb, int N, int64_t P, const float amax_a,
@@ -1824,11 +1812,6 @@ __device__ __forceinline__ void wgrad_dma_body(
                      : (int)((((int64_t)N - 1) * ldb + (P / 16 - 1) * bsb + 16) * 4);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nbA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nbB, 0x00020000);
-  // LIN: a T16 operand's piece (tile t, block h) is its 1 KiB contiguous run
-  // (16 rows x 16 samples, lane l: floats 4l .. 4l + 3), split by its owner
-  // into the same fragment image (split_t16)
-  constexpr bool kLin = NERF_WGRAD_LIN != 0;
-  const bool la = kLin && ta, lb = kLin && tb;
   unsigned voA[4], voB[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1839,16 +1822,6 @@ __device__ __forceinline__ void wgrad_dma_body(
     const int64_t rowb = tb ? Lay::rowpart(rb) : (int64_t)rb * ldb;
     voA[i] = ra < M ? (unsigned)((rowa + (col >> 4) * bsa + (col & 15)) * 4) : (unsigned)nbA;
     voB[i] = rb < N ? (unsigned)((rowb + (col >> 4) * bsb + (col & 15)) * 4) : (unsigned)nbB;
-    if (la) {
-      const int r0 = m0 + 16 * t;
-      voA[i] = r0 < ((M + 15) & ~15) ? (unsigned)((h * bsa + (int64_t)r0 * 16 + 4 * lane) * 4)
-                                     : (unsigned)nbA;
-    }
-    if (lb) {
-      const int r0 = n0 + 16 * t;
-      voB[i] = r0 < ((N + 15) & ~15) ? (unsigned)((h * bsb + (int64_t)r0 * 16 + 4 * lane) * 4)
-                                     : (unsigned)nbB;
-    }
   }
   // piece I of granule g: A (g even) or B (g odd) of step g >> 1, into slot g % 5
   auto issue_piece = [&](int g, auto Ic) {
@@ -1874,43 +1847,6 @@ __device__ __forceinline__ void wgrad_dma_body(
     issue_piece(g, std::integral_constant<int, 3>{});
   };
 
-#if NERF_WGRAD_PF
-  const bool pf_b = wave >= 4;
-  unsigned vpf;
-  {
-    const int u = (wave & 3) * 64 + lane, rows = pf_b ? N : M, r0 = pf_b ? n0 : m0;
-    const int nbx = pf_b ? nbB : nbA;
-    if (pf_b ? tb : ta) {   // T16: a block's rows are contiguous, 64 B each
-      const int b = u & 1, rp = u >> 1;
-      vpf = r0 + 2 * rp < ((rows + 15) & ~15)
-                ? (unsigned)((b * (pf_b ? bsb : bsa) + (int64_t)(r0 + 2 * rp) * 16) * 4)
-                : (unsigned)nbx;
-    } else {
-      const int r = r0 + u;
-      vpf = r < rows ? (unsigned)((int64_t)r * (pf_b ? ldb : lda) * 4) : (unsigned)nbx;
-    }
-  }
-  // the wave's operand as a raw descriptor (base, num_records, flags as rA / rB)
-  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
-  u32x4s rpf;
-  {
-    const uintptr_t base = (uintptr_t)(pf_b ? (const void*)B : (const void*)A);
-    rpf.x = __builtin_amdgcn_readfirstlane((unsigned)base);
-    rpf.y = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
-    rpf.z = __builtin_amdgcn_readfirstlane((unsigned)(pf_b ? nbB : nbA));
-    rpf.w = 0x00020000u;
-  }
-  const int64_t pf_bs = pf_b ? bsb : bsa;
-  const int pf_nb = pf_b ? nbB : nbA;
-  unsigned pf = 0u;   // the dummy destination: one register, live to the final drain
-  auto prefetch = [&](int k) {
-    const int kk = k + NERF_WGRAD_PF;
-    const int so = __builtin_amdgcn_readfirstlane(
-        kk < nsteps ? (int)(((pb + (int64_t)kk * kstride) >> 4) * pf_bs * 4) : pf_nb);
-    asm volatile("buffer_load_dword %0, %1, %2, %3 offen"
-                 : "+v"(pf) : "v"(vpf), "s"(rpf), "s"(so) : "memory");
-  };
-#endif
   const int mb = wave & 3, nb = wave >> 2;   // wave tile: rows 64 mb.., cols 128 nb..
   const bool busy = (m0 + 64 * mb < M) && (n0 + 128 * nb < N);   // wave-uniform
   f32x4 acc[4][8];
@@ -1940,43 +1876,8 @@ __device__ __forceinline__ void wgrad_dma_body(
     q[0] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 0, 1, 2, 3));
     q[64] = __builtin_bit_cast(u32x4, __builtin_shufflevector(v, v, 4, 5, 6, 7));
   };
-  // LIN: lane l holds (slot l >> 2 = row 4 ((l >> 2) & 3) + (l >> 4) of the
-  // tile, samples 4 (l & 3) .. + 3) of each block; hi / lo of the quad go to
-  // fragment lane 16 (2 block + ((l & 3) >> 1)) + row, bytes 8 (l & 1) of its
-  // 16 (the image split_own leaves). The wave owns the whole 2 KiB of the tile
-  // and reads both runs before writing
-  auto split_t16 = [&](int g, int t, float s, bool sum) {
-    const unsigned base = lds_addr((const float*)&ring[g % kWgRing][(2 * (2 * wave + t)) * 64]);
-    const u32x4* q = reinterpret_cast<const u32x4*>(&ring[g % kWgRing][(2 * (2 * wave + t)) * 64 + lane]);
-    const u32x4 x = q[0], y = q[64];
-    Op v = __builtin_bit_cast(Op, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
-    if (sum) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) rs[t] += v[u];
-    }
-    split_op(v, s);   // hi: (b0 q0 q1, b0 q2 q3, b1 .., b1 ..), then lo
-    const int row = 4 * ((lane >> 2) & 3) + (lane >> 4), c = lane & 3;
-    const unsigned d0 = base + (unsigned)(((c >> 1) * 16 + row) * 16 + 8 * (c & 1));
-    const unsigned d1 = d0 + 32u * 16u;   // block 1: fragment lanes 32 ..
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 h0, h1, l0, l1;
-    h0.x = __float_as_uint(v[0]); h0.y = __float_as_uint(v[1]);
-    h1.x = __float_as_uint(v[2]); h1.y = __float_as_uint(v[3]);
-    l0.x = __float_as_uint(v[4]); l0.y = __float_as_uint(v[5]);
-    l1.x = __float_as_uint(v[6]); l1.y = __float_as_uint(v[7]);
-    asm volatile("ds_write_b64 %0, %1" :: "v"(d0), "v"(h0) : "memory");
-    asm volatile("ds_write_b64 %0, %1 offset:1024" :: "v"(d0), "v"(l0) : "memory");
-    asm volatile("ds_write_b64 %0, %1" :: "v"(d1), "v"(h1) : "memory");
-    asm volatile("ds_write_b64 %0, %1 offset:1024" :: "v"(d1), "v"(l1) : "memory");
-  };
-  auto split_a = [&](int g, int t) {
-    if (la) split_t16(g, t, t ? sa1 : sa0, true);
-    else split_own(g, t, t ? sa1 : sa0, true);
-  };
-  auto split_b = [&](int g, int t) {
-    if (lb) split_t16(g, t, sb, false);
-    else split_own(g, t, sb, false);
-  };
+  auto split_a = [&](int g, int t) { split_own(g, t, t ? sa1 : sa0, true); };
+  auto split_b = [&](int g, int t) { split_own(g, t, sb, false); };
 
   // prologue: granules 0 .. 3 (A_0, B_0, A_1, B_1), then this wave's share of step 0
   for (int g = 0; g < 4 && g < ngran; ++g) issue(g);
@@ -2001,23 +1902,17 @@ __device__ __forceinline__ void wgrad_dma_body(
     // (later or earlier splits: within 1.5 %, profiles/r5_wgrad_selfsplit/)
     const int ga = 2 * k + 4, gb = 2 * k + 5;
     const bool nxt = k + 1 < nsteps, nxt2 = k + 2 < nsteps;
-#if NERF_WGRAD_PF
-    constexpr int c = 1;   // the step's prefetch: one more load behind the waited ones
-    prefetch(k);
-#else
-    constexpr int c = 0;
-#endif
     if (!busy) {   // nothing to multiply: stage and split this wave's pieces
       issue(ga);
       __builtin_amdgcn_s_barrier();
       if (nxt) {
-        vm_wait_n((nxt2 ? 8 : 4) + c);
+        vm_wait_n(nxt2 ? 8 : 4);
         split_a(2 * k + 2, 0);
         split_a(2 * k + 2, 1);
       }
       issue(gb);
       if (nxt) {
-        vm_wait_n((nxt2 ? 8 : 0) + c);
+        vm_wait_n(nxt2 ? 8 : 0);
         split_b(2 * k + 3, 0);
         split_b(2 * k + 3, 1);
       }
@@ -2058,8 +1953,8 @@ __device__ __forceinline__ void wgrad_dma_body(
 #endif
       }
       if (nxt) {   // after B_{k+2} piece j - 4: A_{k+1} needs 9 (4) newer in flight, B_{k+1} 7 (0)
-        if constexpr (j == 4) vm_wait_n((nxt2 ? 9 : 4) + c);
-        if constexpr (j == 6) vm_wait_n((nxt2 ? 7 : 0) + c);
+        if constexpr (j == 4) vm_wait_n(nxt2 ? 9 : 4);
+        if constexpr (j == 6) vm_wait_n(nxt2 ? 7 : 0);
         if constexpr (j == 4 || j == 5) split_a(2 * k + 2, j - 4);
         if constexpr (j == 6 || j == 7) split_b(2 * k + 3, j - 6);
       }
@@ -2073,24 +1968,14 @@ __device__ __forceinline__ void wgrad_dma_body(
     tile(std::integral_constant<int, 6>{});
     tile(std::integral_constant<int, 7>{});
   }
-#if NERF_WGRAD_PF
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf) : : "memory");   // no load left in flight
-#endif
   if (bias_part && ntile == 0) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 2; ++t) {   // row 16 (2 wave + t) + (l & 15): lanes l, l^16, l^32, l^48
       float r = rs[t];
-      if (la) {   // row 16 (2 wave + t) + 4 ((l >> 2) & 3) + (l >> 4): lanes l, l^1, l^2, l^3
-        r += __shfl_xor(r, 1);
-        r += __shfl_xor(r, 2);
-        const int row = m0 + 16 * (2 * wave + t) + 4 * ((lane >> 2) & 3) + (lane >> 4);
-        if ((lane & 3) == 0 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
-      } else {    // row 16 (2 wave + t) + (l & 15): lanes l, l^16, l^32, l^48
-        r += __shfl_xor(r, 16);
-        r += __shfl_xor(r, 32);
-        const int row = m0 + 16 * (2 * wave + t) + lane;
-        if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
-      }
+      r += __shfl_xor(r, 16);
+      r += __shfl_xor(r, 32);
+      const int row = m0 + 16 * (2 * wave + t) + lane;
+      if (lane < 16 && row < M) bias_part[(int64_t)z * ldbias + row] = r;
     }
   }
   if (!busy) return;
