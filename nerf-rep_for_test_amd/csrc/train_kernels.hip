@@ -549,73 +549,79 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 //   dW_views = [Gh W_f^T + s b_f^T, GA[0:128, 256:283]],  db_views = s,
 //   dW_f = W_views[:, :256]^T Gh,  db_f = W_views[:, :256]^T s,
 //   dW_alpha = GA[128, 0:256],  db_alpha = ba[128].
-// One thread per output element, float32 sums in k order (one launch in place
-// of two small hipBLASLt GEMMs, a GEMV and the copies around them); vec: GA's
-// rows and W_f 16-B aligned.
-constexpr int kVfViews = 128 * 283, kVfFeat = 256 * 256;
-constexpr int kVfTotal = kVfViews + kVfFeat + 256 + 256 + 1 + 128;
+// One launch in place of two small hipBLASLt GEMMs, a GEMV and the copies
+// around them. The two products run as 32 x 32 output tiles (dW_views,feat:
+// 4 x 8 tiles over K = 256; dW_f: 8 x 8 over K = 128), both operands' whole K
+// extent staged through LDS at once (every load of a thread in flight
+// together: a chunked K loop exposed one load latency per chunk), each thread
+// 2 x 2 outputs, every output one FP32 FMA chain in ascending k (the order of
+// a one-thread-per-output loop); one more workgroup takes db_f (a GEMV,
+// ascending i) and the copies.
+constexpr int kVfTilesV = 4 * 8, kVfTilesF = 8 * 8;
 __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     const float* __restrict__ GA, int64_t ldga, const float* __restrict__ ba,
     const float* __restrict__ Wf, const float* __restrict__ bf, const float* __restrict__ Wv,
     float* __restrict__ dWv, float* __restrict__ dWf, float* __restrict__ dbf,
-    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv, bool vec) {
-  int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (t >= kVfTotal) return;
-  if (t < kVfViews) {
-    const int i = t / 283, j = t % 283;
-    const float* g = GA + (int64_t)i * ldga;
-    if (j >= 256) {
-      dWv[t] = g[j];
-      return;
-    }
-    const float* w = Wf + (int64_t)j * 256;
+    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv) {
+  const int t = threadIdx.x;
+  const int blk = blockIdx.x;
+  if (blk == kVfTilesV + kVfTilesF) {   // db_f, the copies
     float acc = 0.0f;
-    if (vec) {   // 16-B loads (4 k per load; the lanes' W_f rows are 1 KiB apart)
-      const float4* g4 = reinterpret_cast<const float4*>(g);
-      const float4* w4 = reinterpret_cast<const float4*>(w);
-#pragma unroll 16
-      for (int k = 0; k < 64; ++k) {
-        const float4 a = g4[k], b = w4[k];
-        acc = __builtin_fmaf(a.x, b.x, acc);
-        acc = __builtin_fmaf(a.y, b.y, acc);
-        acc = __builtin_fmaf(a.z, b.z, acc);
-        acc = __builtin_fmaf(a.w, b.w, acc);
-      }
-    } else {
-      for (int k = 0; k < 256; ++k) acc = __builtin_fmaf(g[k], w[k], acc);
-    }
-    dWv[t] = __builtin_fmaf(ba[i], bf[j], acc);
-    return;
-  }
-  t -= kVfViews;
-  if (t < kVfFeat) {
-    const int a = t >> 8, b = t & 255;
-    float acc = 0.0f;
-#pragma unroll 16
-    for (int i = 0; i < 128; ++i)
-      acc = __builtin_fmaf(Wv[(int64_t)i * 283 + a], GA[(int64_t)i * ldga + b], acc);
-    dWf[t] = acc;
-    return;
-  }
-  t -= kVfFeat;
-  if (t < 256) {
-    float acc = 0.0f;
-#pragma unroll 16
+#pragma unroll 32
     for (int i = 0; i < 128; ++i) acc = __builtin_fmaf(Wv[(int64_t)i * 283 + t], ba[i], acc);
     dbf[t] = acc;
-    return;
-  }
-  t -= 256;
-  if (t < 256) {
     dWa[t] = GA[128 * ldga + t];
+    if (t < 128) dbv[t] = ba[t];
+    if (t == 0) dba[0] = ba[128];
+    for (int e = t; e < 128 * 27; e += 256) {
+      const int i = e / 27, j = 256 + e % 27;
+      dWv[i * 283 + j] = GA[(int64_t)i * ldga + j];
+    }
     return;
   }
-  t -= 256;
-  if (t == 0) {
-    dba[0] = ba[128];
-    return;
+  // C[m][n] = sum_k A(m, k) B(k, n) over a 32 x 32 tile
+  const bool views = blk < kVfTilesV;
+  const int tile = views ? blk : blk - kVfTilesV;
+  const int m0 = 32 * (tile >> 3), n0 = 32 * (tile & 7);
+  const int K = views ? 256 : 128;
+  __shared__ float As[256][33], Bs[256][33];   // As[k][m], Bs[k][n]
+  const int tm = t >> 4, tn = t & 15;          // outputs (m0 + 2 tm + a, n0 + 2 tn + b)
+  if (views) {
+    // A(m, k) = GA[m][k], B(k, n) = W_f[n][k] (k contiguous): 32 rows x 256 k each
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) {
+      const int e = t + 256 * q, r = e >> 8, c = e & 255;
+      As[c][r] = GA[(int64_t)(m0 + r) * ldga + c];
+      Bs[c][r] = Wf[(int64_t)(n0 + r) * 256 + c];
+    }
+  } else {
+    // A(m, k) = W_views[k][m], B(k, n) = GA[k][n] (m / n contiguous): 128 k x 32
+#pragma unroll 8
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, r = e >> 5, c = e & 31;
+      As[r][c] = Wv[(int64_t)r * 283 + m0 + c];
+      Bs[r][c] = GA[(int64_t)r * ldga + n0 + c];
+    }
   }
-  dbv[t - 1] = ba[t - 1];
+  __syncthreads();
+  float acc[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+#pragma unroll 8
+  for (int k = 0; k < K; ++k) {
+    const float a0 = As[k][2 * tm], a1 = As[k][2 * tm + 1];
+    const float b0 = Bs[k][2 * tn], b1 = Bs[k][2 * tn + 1];
+    acc[0][0] = __builtin_fmaf(a0, b0, acc[0][0]);
+    acc[0][1] = __builtin_fmaf(a0, b1, acc[0][1]);
+    acc[1][0] = __builtin_fmaf(a1, b0, acc[1][0]);
+    acc[1][1] = __builtin_fmaf(a1, b1, acc[1][1]);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int m = m0 + 2 * tm + a, n = n0 + 2 * tn + b;
+      if (views) dWv[m * 283 + n] = __builtin_fmaf(ba[m], bf[n], acc[a][b]);
+      else dWf[m * 256 + n] = acc[a][b];
+    }
 }
 
 int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, const float* Wf,
@@ -623,9 +629,8 @@ int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, con
                              float* dWa, float* dba, float* dbv, nerf_stream_t stream) {
   NERF_REQUIRE(GA && ba && Wf && bf && Wv && dWv && dWf && dbf && dWa && dba && dbv && ldga >= 283,
                "nerf_views_feature_grads: bad arguments");
-  hipLaunchKernelGGL(views_feature_grads_kernel, dim3((unsigned)cdiv(kVfTotal, 256)), dim3(256), 0,
-                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv,
-                     ((uintptr_t)GA | (uintptr_t)Wf | (uintptr_t)(ldga * 4)) % 16 == 0);
+  hipLaunchKernelGGL(views_feature_grads_kernel, dim3(kVfTilesV + kVfTilesF + 1), dim3(256), 0,
+                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv);
   return check_launch("views_feature_grads_kernel");
 }
 
@@ -653,7 +658,9 @@ int nerf_adam_step(const NerfAdamTensor* tensors, int n, const float* lr, float*
 //   m = m + (1 - b1) (g - m),  v = v b2 + (1 - b2) g g,
 //   p = p - lr / (1 - b1^t) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)),  t = step + 1.
 // lr and the step count live on the device (a HIP graph replays the launch);
-// adam_advance_kernel then writes step = t.
+// adam_advance_kernel then writes step = t (an arrival counter letting the
+// last workgroup write it measured slower: ~1 200 workgroups' atomics on one
+// word, 21 vs 13 + 5 µs).
 constexpr int kAdamMax = 64;
 constexpr int kAdamPer = 4;                 // elements per thread, loaded together
 constexpr int kAdamBlock = 256 * kAdamPer;  // elements per workgroup (~1 200 workgroups for
@@ -685,6 +692,7 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch b, const floa
   const float step_size = (float)((double)*lr / (1.0 - pow(beta1, (double)t)));
   const float bc2s = (float)sqrt(1.0 - pow(beta2, (double)t));
   const float w1 = (float)(1.0 - beta1), w2 = (float)(1.0 - beta2), b2 = (float)beta2;
+
   float g[kAdamPer], m0[kAdamPer], v0[kAdamPer], p0[kAdamPer];
 #pragma unroll
   for (int r = 0; r < kAdamPer; ++r) {

@@ -417,7 +417,12 @@ class NerfTrainer:
         one = self._one.get(loss.device)
         if one is None:   # d loss / d loss = 1, kept (no fill kernel per step)
             one = self._one[loss.device] = torch.ones((), device=loss.device, dtype=loss.dtype)
-        loss.backward(one)
+        if self.mlp == "x3":   # one fused node per network: the weight gradients on a side stream
+            from .train_mlp import side_wgrad_scope
+            with side_wgrad_scope(self.fine is None or self.fine is not self.coarse):
+                loss.backward(one)
+        else:
+            loss.backward(one)
         if group is not None:
             allreduce_mean([p.grad for p in self.trained_parameters()], group)
         if self.adam != "hip":   # (HipAdam clamps the gradients itself, in place)

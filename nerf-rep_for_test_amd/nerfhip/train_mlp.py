@@ -1122,6 +1122,42 @@ class NerfMLPFn(torch.autograd.Function):
             post[s] = (f"pts_linears.{i}.weight", f"pts_linears.{i}.bias", None)
             if i == 5:
                 post[wb.add(D[5], H[4], dmax[5:6], amax[4:5], into=(s, 63))] = None
+        # the weight gradients need nothing of the rest of the backward: with the
+        # fused kernels they run on a side stream, so the launches after this
+        # node (the fine network's d z -> sample_pdf / composite backward of the
+        # coarse one) overlap them; the main stream joins at the end of the pass
+        side = _side_stream(dev) if ctx.fused_backward and SIDE_WGRAD and _SIDE_SCOPE[0] else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            NerfMLPFn._weight_grads(wb, post, grads, heads_merged, v_h7, p, dev)
+        if side is not None:
+            _join_side(side, wb, grads, (amax, dmax), params, dev)
+        d_pts = None
+        if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
+            def lay(t):   # (row stride, T16 block stride) of an operand
+                return (BLOCK, t.block_stride) if isinstance(t, BlockRows) else (t.stride(0), 0)
+            assert lay(d_enc[0]) == lay(d_enc[1])
+            (ldd, bsd), (lde, bse) = lay(d_enc[0]), lay(E)
+            if rays_S:          # pts = the rays' o + d z: straight on to d z
+                d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
+                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                     ptr(E), lde, bse, ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
+                     _lib.stream_of(dev))
+            else:
+                d_pts = torch.empty((P, 3), device=dev, dtype=f32)
+                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                     ptr(E), lde, bse, ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
+                     _lib.stream_of(dev))
+        if rays_S:
+            return (None, None, d_pts, *[grads[n] for n in PARAM_NAMES])
+        return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
+
+    @staticmethod
+    def _weight_grads(wb, post, grads, heads_merged, v_h7, p, dev):
+        """The batched weight-gradient launch and its post-processing (the views /
+        feature / alpha gradients through G) on the current stream."""
+        f32 = torch.float32
         for slot, res in enumerate(wb.results()):
             if post[slot] is None:   # a column block joined into another slot's result
                 continue
@@ -1158,25 +1194,79 @@ class NerfMLPFn(torch.autograd.Function):
                              p["feature_linear.weight"].t()), G[:, 256:283]], 1)
             grads["feature_linear.weight"] = Wvf.t() @ Gh
             grads["feature_linear.bias"] = Wvf.t() @ sv
-        d_pts = None
-        if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
-            def lay(t):   # (row stride, T16 block stride) of an operand
-                return (BLOCK, t.block_stride) if isinstance(t, BlockRows) else (t.stride(0), 0)
-            assert lay(d_enc[0]) == lay(d_enc[1])
-            (ldd, bsd), (lde, bse) = lay(d_enc[0]), lay(E)
-            if rays_S:          # pts = the rays' o + d z: straight on to d z
-                d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
-                     ptr(E), lde, bse, ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
-                     _lib.stream_of(dev))
-            else:
-                d_pts = torch.empty((P, 3), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
-                     ptr(E), lde, bse, ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
-                     _lib.stream_of(dev))
-        if rays_S:
-            return (None, None, d_pts, *[grads[n] for n in PARAM_NAMES])
-        return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
+
+
+# NERF_TRAIN_SIDE_WGRAD=0: the weight gradients on the main stream, in line
+SIDE_WGRAD = _os.environ.get("NERF_TRAIN_SIDE_WGRAD", "1") != "0"
+_SIDE = {}
+_SIDE_SCOPE = [False]   # a plain global: the autograd engine runs backward on its own thread
+
+
+class side_wgrad_scope:
+    """Backward passes inside this scope may compute the fused MLPs' weight
+    gradients on a side stream (joined at the end of the pass). Only for
+    passes in which every parameter receives ONE gradient, into a .grad that
+    is None (NerfTrainer: one fused node per network, zero_grad(set_to_none)):
+    a second gradient for the same parameter would be added on the main stream
+    before the join."""
+
+    def __init__(self, on=True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = _SIDE_SCOPE[0]
+        _SIDE_SCOPE[0] = self.on
+        return self
+
+    def __exit__(self, *a):
+        _SIDE_SCOPE[0] = self.prev
+        return False
+
+
+def _side_stream(dev):
+    s = _SIDE.get(str(dev))
+    if s is None:
+        s = _SIDE[str(dev)] = torch.cuda.Stream(dev)
+    return s
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+def _join_side(side, wb, grads, stats, params, dev):
+    """After the side-stream weight gradients: every buffer they read stays
+    allocated until they are done (record_stream), the gradients are handed to
+    the main stream, which waits for them at the end of the backward pass (an
+    engine callback) -- or at once when a parameter already holds a gradient
+    (AccumulateGrad then adds into it right away)."""
+    main = torch.cuda.current_stream(dev)
+
+    def keep(t):
+        if isinstance(t, tuple):
+            for u in t:
+                keep(u)
+        elif isinstance(t, BlockRows):
+            t.buf.record_stream(side)
+        elif isinstance(t, torch.Tensor):
+            t.record_stream(side)
+    for r in wb.req:
+        for t in r[:4]:
+            keep(t)
+    for t in stats:
+        keep(t)
+    for g in grads.values():
+        g.record_stream(main)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    if any(q.grad is not None for q in params):
+        main.wait_event(ev)
+    else:
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_event(ev))
 
 
 def _backward_layers_impl(DR, p, pk, bits, bits_v, dmax, need_enc):

@@ -379,6 +379,35 @@ def test_graph_step_equals_eager_steps(dev, explicit_draws):
     assert np.all(np.abs(lf[:2] - lh[:2]) <= 1e-5 * np.abs(lf[:2])), (lf, lh)
 
 
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_side_stream_weight_grads_equal_inline(dev, mode, monkeypatch):
+    """NerfTrainer's backward computes the fused MLPs' weight gradients on a side
+    stream (train_mlp.side_wgrad_scope; joined at the end of the pass) while
+    the main stream runs on through the fine d z and the coarse backward: 5
+    steps give bitwise the losses and parameters of the in-line schedule
+    (NERF_TRAIN_SIDE_WGRAD=0), eager and as a HIP graph -- a read of a
+    gradient before the join, or a buffer reused while the side stream still
+    reads it, would show."""
+    from nerfhip import train_mlp
+    from nerfhip.train import NerfTrainer
+    z, _, ro, rd, _, _, gt = _setup(dev, "x3")
+    g = torch.Generator(device=dev).manual_seed(3)
+    n = ro.shape[0]
+    batches = [(ro[p], rd[p], gt[p], torch.rand((n, 64), device=dev, generator=g),
+                torch.rand((n, 128), device=dev, generator=g))
+               for p in (torch.randperm(n, device=dev, generator=g) for _ in range(5))]
+    runs = {}
+    for side in (False, True):
+        monkeypatch.setattr(train_mlp, "SIDE_WGRAD", side)
+        tr = NerfTrainer(dev, params_of(z), mlp="x3", graph=mode == "graph")
+        losses = [float(tr.step(*b)["loss"].item()) for b in batches]
+        runs[side] = (np.array(losses), {k: v.clone() for k, v in tr.state().items()})
+    assert np.array_equal(runs[False][0], runs[True][0]), runs
+    for k, a in runs[False][1].items():
+        assert torch.equal(a, runs[True][1][k]), k
+    assert not train_mlp._SIDE_SCOPE[0]
+
+
 def test_hip_adam_matches_torch_adam(dev):
     """HipAdam (clip_grad_value_ + Adam in one nerf_adam_step launch) against
     torch.optim.Adam (foreach=False) after torch's clip_grad_value_, 6 steps on

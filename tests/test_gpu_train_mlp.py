@@ -704,3 +704,36 @@ def test_ray_form_equals_point_form(dev, n, S):
     dz, dz_ref = got_g[0], ref_g[0]
     assert dz.shape == (n, S)
     assert float((dz - dz_ref).abs().max()) <= 1e-6 * float(dz_ref.abs().max().clamp_min(1e-30))
+
+
+def test_views_feature_grads_kernel_matches_float64(dev):
+    """nerf_views_feature_grads (the views / feature / alpha gradients from the
+    merged G tile): dW_views = [Gh W_f^T + s b_f^T, G_enc], dW_f = W_vf^T Gh,
+    db_f = W_vf^T s, the alpha row and the bias copies, against float64 torch
+    within 1e-6 of each output's scale (row stride of GA > 288)."""
+    from nerfhip._lib import call, ptr, stream_of
+    g = torch.Generator(device=dev).manual_seed(21)
+    ld = 300
+    GA = torch.randn((129, ld), device=dev, generator=g)
+    ba = torch.randn((129,), device=dev, generator=g)
+    Wf = torch.randn((256, 256), device=dev, generator=g) * 0.1
+    bf = torch.randn((256,), device=dev, generator=g)
+    Wv = torch.randn((128, 283), device=dev, generator=g) * 0.1
+    out = {k: torch.full(s, float("nan"), device=dev) for k, s in (
+        ("dWv", (128, 283)), ("dWf", (256, 256)), ("dbf", (256,)), ("dWa", (1, 256)),
+        ("dba", (1,)), ("dbv", (128,)))}
+    call("nerf_views_feature_grads", ptr(GA), ld, ptr(ba), ptr(Wf), ptr(bf), ptr(Wv),
+         ptr(out["dWv"]), ptr(out["dWf"]), ptr(out["dbf"]), ptr(out["dWa"]), ptr(out["dba"]),
+         ptr(out["dbv"]), stream_of(dev))
+    d = {k: v.double() for k, v in (("GA", GA), ("ba", ba), ("Wf", Wf), ("bf", bf), ("Wv", Wv))}
+    Gh, s = d["GA"][:128, :256], d["ba"][:128]
+    ref = {"dWv": torch.cat([Gh @ d["Wf"].t() + s[:, None] * d["bf"][None, :],
+                             d["GA"][:128, 256:283]], 1),
+           "dWf": d["Wv"][:, :256].t() @ Gh, "dbf": d["Wv"][:, :256].t() @ s,
+           "dWa": d["GA"][128:129, :256], "dba": d["ba"][128:129], "dbv": s}
+    scale = {"dWv": (Gh.abs() @ d["Wf"].abs().t() + (s[:, None] * d["bf"][None, :]).abs()).max(),
+             "dWf": (d["Wv"][:, :256].abs().t() @ Gh.abs()).max(),
+             "dbf": (d["Wv"][:, :256].abs().t() @ s.abs()).max()}
+    for k, r in ref.items():
+        e = float((out[k].double() - r).abs().max())
+        assert e <= 1e-6 * float(scale.get(k, 1.0)), (k, e)
