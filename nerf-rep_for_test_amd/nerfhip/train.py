@@ -417,9 +417,11 @@ class NerfTrainer:
         one = self._one.get(loss.device)
         if one is None:   # d loss / d loss = 1, kept (no fill kernel per step)
             one = self._one[loss.device] = torch.ones((), device=loss.device, dtype=loss.dtype)
-        if self.mlp == "x3":   # one fused node per network: the weight gradients on a side stream
+        if self.mlp == "x3" and self.N_importance > 0 and self.fine is not self.coarse:
+            # one fused node per network: the fine network's weight gradients on a
+            # side stream while the main one runs on through the coarse backward
             from .train_mlp import side_wgrad_scope
-            with side_wgrad_scope(self.fine is None or self.fine is not self.coarse):
+            with side_wgrad_scope([self.fine]):
                 loss.backward(one)
         else:
             loss.backward(one)

@@ -1126,7 +1126,9 @@ class NerfMLPFn(torch.autograd.Function):
         # fused kernels they run on a side stream, so the launches after this
         # node (the fine network's d z -> sample_pdf / composite backward of the
         # coarse one) overlap them; the main stream joins at the end of the pass
-        side = _side_stream(dev) if ctx.fused_backward and SIDE_WGRAD and _SIDE_SCOPE[0] else None
+        side = _side_stream(dev) if (ctx.fused_backward and SIDE_WGRAD and
+                                     p["pts_linears.0.weight"].data_ptr() in _SIDE_SCOPE[0]) \
+            else None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side) if side is not None else _nullctx():
@@ -1199,19 +1201,27 @@ class NerfMLPFn(torch.autograd.Function):
 # NERF_TRAIN_SIDE_WGRAD=0: the weight gradients on the main stream, in line
 SIDE_WGRAD = _os.environ.get("NERF_TRAIN_SIDE_WGRAD", "1") != "0"
 _SIDE = {}
-_SIDE_SCOPE = [False]   # a plain global: the autograd engine runs backward on its own thread
+_SIDE_SCOPE = [frozenset()]   # a plain global: the autograd engine runs backward on its own thread
 
 
 class side_wgrad_scope:
-    """Backward passes inside this scope may compute the fused MLPs' weight
-    gradients on a side stream (joined at the end of the pass). Only for
-    passes in which every parameter receives ONE gradient, into a .grad that
-    is None (NerfTrainer: one fused node per network, zero_grad(set_to_none)):
-    a second gradient for the same parameter would be added on the main stream
-    before the join."""
+    """Backward passes inside this scope compute the weight gradients of the
+    given networks' fused MLP nodes on a side stream (joined at the end of the
+    pass), so the main stream runs on meanwhile -- worth it for a network whose
+    backward has work after it (NerfTrainer: the fine network; the coarse one
+    is last, and a side stream would only add two cross-queue waits). Only for
+    passes in which each of those parameters receives ONE gradient, into a
+    .grad that is None (NerfTrainer: one fused node per network,
+    zero_grad(set_to_none)): a second gradient for the same parameter would be
+    added on the main stream before the join. networks: modules or their first
+    weight tensors."""
 
-    def __init__(self, on=True):
-        self.on = bool(on)
+    def __init__(self, networks=()):
+        keys = set()
+        for n in networks:
+            w = mlp_params(n)[0] if isinstance(n, torch.nn.Module) else n
+            keys.add(w.data_ptr())
+        self.on = frozenset(keys)
 
     def __enter__(self):
         self.prev = _SIDE_SCOPE[0]
