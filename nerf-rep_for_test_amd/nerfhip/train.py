@@ -411,7 +411,7 @@ class NerfTrainer:
         self.opt.zero_grad(set_to_none=True)
         if self.mlp == "x3":   # both networks' weight streams in one packing launch set
             from .train_mlp import prepack
-            prepack([self.coarse] + ([self.fine] if self.N_importance > 0 else []))
+            prepack([self.coarse] + ([self.fine] if self.N_importance > 0 else []), side=True)
         losses = self.loss(self.forward(rays_o, rays_d, t_rand, u), target)
         loss = losses["loss"]
         one = self._one.get(loss.device)

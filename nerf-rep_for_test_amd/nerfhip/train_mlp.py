@@ -381,6 +381,7 @@ class X3NetPacker:
         self.bwd = X3BwdStreamPacker(device)
         self.key = None         # storage key of the built tables
         self.pending = False    # packed by prepack() for the next streams() call
+        self.pending_event = None   # prepack(side=True): the pack stream's completion
 
     def _ensure_built(self, p):
         key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
@@ -399,11 +400,17 @@ class X3NetPacker:
         self._ensure_built(p)
         if not self.pending:
             _launch_packs([self])
+        elif self.pending_event is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.pending_event)
         self.pending = False
+        self.pending_event = None
         return self.fwd.stream, self.fwd.head, self.bwd.stream, self.bwd.head
 
     def invalidate(self):
+        if self.pending_event is not None:   # a side-stream packing still writing the buffers
+            torch.cuda.current_stream(self.device).wait_event(self.pending_event)
         self.pending = False
+        self.pending_event = None
 
 
 _PACK_TABLES = {}
@@ -442,11 +449,14 @@ def _net_for(params, device):
     return net, p
 
 
-def prepack(networks):
+def prepack(networks, side=False):
     """Pack the fused kernels' streams of several networks (each a list of its
     24 parameters in PARAM_NAMES order, or a NeRF module) in ONE launch set;
     each network's next forward uses them instead of packing (a training step
-    calls it right before its forwards, after the previous optimizer step)."""
+    calls it right before its forwards, after the previous optimizer step).
+    side=True: the launch set runs on a side stream (after everything already
+    on the current one), and each network's next forward makes its stream
+    wait for it -- the launches between (draws, coarse depths) overlap it."""
     nets = []
     for params in networks:
         if isinstance(params, torch.nn.Module):
@@ -455,9 +465,20 @@ def prepack(networks):
         net._ensure_built(p)
         nets.append(net)
     if nets:
-        _launch_packs(nets)
+        ev = None
+        if side:
+            dev = nets[0].device
+            ps = _side_stream(dev, "pack")
+            ps.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(ps):
+                _launch_packs(nets)
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        else:
+            _launch_packs(nets)
         for n in nets:
             n.pending = True
+            n.pending_event = ev
 
 
 def invalidate_packs():
@@ -1233,10 +1254,10 @@ class side_wgrad_scope:
         return False
 
 
-def _side_stream(dev):
-    s = _SIDE.get(str(dev))
+def _side_stream(dev, role="wgrad"):
+    s = _SIDE.get((str(dev), role))
     if s is None:
-        s = _SIDE[str(dev)] = torch.cuda.Stream(dev)
+        s = _SIDE[(str(dev), role)] = torch.cuda.Stream(dev)
     return s
 
 
