@@ -382,6 +382,10 @@ class X3NetPacker:
         self.key = None         # storage key of the built tables
         self.pending = False    # packed by prepack() for the next streams() call
         self.pending_event = None   # prepack(side=True): the pack stream's completion
+        # prepack(side=True) also zeroes the max |.| slots of the network's next
+        # forward + backward (RayMLPFn) on the pack stream: handed out once
+        self.stats = None
+        self.stats_ready = False
 
     def _ensure_built(self, p):
         key = tuple((k, v.data_ptr()) for k, v in sorted(p.items()))
@@ -406,7 +410,15 @@ class X3NetPacker:
         self.pending_event = None
         return self.fwd.stream, self.fwd.head, self.bwd.stream, self.bwd.head
 
+    def take_stats(self):
+        """The slots prepack zeroed for this network's next forward, or None."""
+        if not (self.pending and self.stats_ready):
+            return None
+        self.stats_ready = False
+        return self.stats
+
     def invalidate(self):
+        self.stats_ready = False
         if self.pending_event is not None:   # a side-stream packing still writing the buffers
             torch.cuda.current_stream(self.device).wait_event(self.pending_event)
         self.pending = False
@@ -472,6 +484,11 @@ def prepack(networks, side=False):
             ps.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(ps):
                 _launch_packs(nets)
+                for n in nets:
+                    if n.stats is None:
+                        n.stats = torch.empty(25, device=dev, dtype=torch.float32)
+                    n.stats.zero_()
+                    n.stats_ready = True
             ev = torch.cuda.Event()
             ev.record(ps)
         else:
@@ -1409,7 +1426,12 @@ class RayMLPFn(torch.autograd.Function):
         n, S = z.shape
         P = n * S
         dev = z.device
-        stats = torch.zeros(25, device=dev, dtype=torch.float32)   # amax + the backward's dmax
+        # amax + the backward's dmax: zeroed by prepack(side=True) for the trainer's
+        # one forward per network and step, else one fill here
+        net, _ = _net_for(params, dev)
+        stats = net.take_stats()
+        if stats is None:
+            stats = torch.zeros(25, device=dev, dtype=torch.float32)
         amax, ctx.dmax_buf = stats[:12], stats[12:]
         ctx.fused_backward = FUSED_BACKWARD and P > 0
         if ctx.fused_backward and _t16_ok(P):   # every row in one T16 buffer (_forward_fused)
