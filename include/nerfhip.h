@@ -42,8 +42,9 @@ const char* nerf_last_error(void);
  * bsa / bsb, NerfX3TrainOut.bs / NerfX3BwdIO.bs and the encoding-backward layout
  * arguments: the T16 activation layout of round 5; 4: NerfWgradDesc.a2_row; 5: the
  * training forward's 65-slice (folded) stream, nerf_fold_views; 6: the backward's
- * 64-slice (folded) stream, NerfX3BwdIO.d[8] NULL) */
-#define NERF_ABI_VERSION 6
+ * 64-slice (folded) stream, NerfX3BwdIO.d[8] NULL; 7: nerf_views_feature_grads
+ * GE / ldge) */
+#define NERF_ABI_VERSION 7
 int nerf_version(void);
 /* 16 hex digits of sha256(the csrc/ files in byte order, then include/nerfhip.h): the
  * source tree this library was compiled from (nerfhip/_lib.py refuses a
@@ -164,10 +165,17 @@ int nerf_sum_partials(const float* part, int64_t C, int64_t n, float* out, nerf_
  * GA[0:128, 256:283]], dWf [256][256] = W_v[:, :256]^T Gh, dbf [256] =
  * W_v[:, :256]^T s, dWa [256] = GA[128, 0:256], dba [1] = ba[128], dbv [128] =
  * s (Gh = GA[0:128, 0:256], s = ba[0:128]; W_f [256][256], b_f [256],
- * W_v [128][283] row-major). */
+ * W_v [128][283] row-major). GE non-NULL (ABI 7): GE = [d_hv; d sigma; pad;
+ * d rgb] [view enc; HV]^T ([147][160+], row stride ldge >= 160) and be its row
+ * sums: the view-encoding columns come from GE[0:128, 0:27] instead of GA (GA
+ * needs only its 256 h7 columns, ldga >= 256), and the rgb head's gradient is
+ * copied out of it too: dWr [3][128] = GE[144:147, 32:160], dbr [3] =
+ * be[144:147] (the training backward's shared tile, nerfhip.train_mlp). GE NULL:
+ * be, dWr, dbr unused. */
 int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, const float* Wf,
                              const float* bf, const float* Wv, float* dWv, float* dWf, float* dbf,
-                             float* dWa, float* dba, float* dbv, nerf_stream_t stream);
+                             float* dWa, float* dba, float* dbv, const float* GE, int64_t ldge,
+                             const float* be, float* dWr, float* dbr, nerf_stream_t stream);
 /* trainers/nerf.py:39-76: out[0] = mean((a - target)^2), out[1] = the same of b
  * (0 when b is NULL), out[2] = out[0] + out[1] (a, b, target: N floats; one
  * workgroup). Backward: g0, g1, g2 = d out[0..2] (device scalars, each nullable

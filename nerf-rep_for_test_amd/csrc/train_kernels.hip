@@ -562,7 +562,9 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     const float* __restrict__ GA, int64_t ldga, const float* __restrict__ ba,
     const float* __restrict__ Wf, const float* __restrict__ bf, const float* __restrict__ Wv,
     float* __restrict__ dWv, float* __restrict__ dWf, float* __restrict__ dbf,
-    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv) {
+    float* __restrict__ dWa, float* __restrict__ dba, float* __restrict__ dbv,
+    const float* __restrict__ GE, int64_t ldge, const float* __restrict__ be,
+    float* __restrict__ dWr, float* __restrict__ dbr) {
   const int t = threadIdx.x;
   const int blk = blockIdx.x;
   if (blk == kVfTilesV + kVfTilesF) {   // db_f, the copies
@@ -574,8 +576,13 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
     if (t < 128) dbv[t] = ba[t];
     if (t == 0) dba[0] = ba[128];
     for (int e = t; e < 128 * 27; e += 256) {
-      const int i = e / 27, j = 256 + e % 27;
-      dWv[i * 283 + j] = GA[(int64_t)i * ldga + j];
+      const int i = e / 27, j = e % 27;
+      dWv[i * 283 + 256 + j] = GE ? GE[(int64_t)i * ldge + j] : GA[(int64_t)i * ldga + 256 + j];
+    }
+    if (GE) {   // the rgb head from the shared tile: rows 144..146 x columns 32..159
+      for (int e = t; e < 3 * 128; e += 256)
+        dWr[e] = GE[(int64_t)(144 + e / 128) * ldge + 32 + e % 128];
+      if (t < 3) dbr[t] = be[144 + t];
     }
     return;
   }
@@ -626,11 +633,14 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
 
 int nerf_views_feature_grads(const float* GA, int64_t ldga, const float* ba, const float* Wf,
                              const float* bf, const float* Wv, float* dWv, float* dWf, float* dbf,
-                             float* dWa, float* dba, float* dbv, nerf_stream_t stream) {
-  NERF_REQUIRE(GA && ba && Wf && bf && Wv && dWv && dWf && dbf && dWa && dba && dbv && ldga >= 283,
+                             float* dWa, float* dba, float* dbv, const float* GE, int64_t ldge,
+                             const float* be, float* dWr, float* dbr, nerf_stream_t stream) {
+  NERF_REQUIRE(GA && ba && Wf && bf && Wv && dWv && dWf && dbf && dWa && dba && dbv &&
+                   ldga >= (GE ? 256 : 283) && (!GE || (ldge >= 160 && be && dWr && dbr)),
                "nerf_views_feature_grads: bad arguments");
   hipLaunchKernelGGL(views_feature_grads_kernel, dim3(kVfTilesV + kVfTilesF + 1), dim3(256), 0,
-                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv);
+                     as_stream(stream), GA, ldga, ba, Wf, bf, Wv, dWv, dWf, dbf, dWa, dba, dbv,
+                     GE, ldge, be, dWr, dbr);
   return check_launch("views_feature_grads_kernel");
 }
 

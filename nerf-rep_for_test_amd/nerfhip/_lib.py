@@ -10,7 +10,7 @@ import os
 import threading
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ABI_VERSION = 6   # include/nerfhip.h NERF_ABI_VERSION
+ABI_VERSION = 7   # include/nerfhip.h NERF_ABI_VERSION
 LIB_PATH = os.environ.get("NERFHIP_LIB", os.path.join(PKG_ROOT, "lib", "libnerfhip.so"))
 
 MLP_SLICES = 73
@@ -47,7 +47,8 @@ SIGNATURES = {
     "nerf_composite_train_fwd": (_I, [_P, _P, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _P, _S]),
     "nerf_composite_train_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I, _I, _P, _P, _P, _P,
                                       _P, _P, _P, _S]),
-    "nerf_views_feature_grads": (_I, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _S]),
+    "nerf_views_feature_grads": (_I, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                      _P, _P, _P, _S]),
     "nerf_mse_pair": (_I, [_P, _P, _P, _I64, _P, _S]),
     "nerf_mse_pair_backward": (_I, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _S]),
     "nerf_sample_pdf_bwd": (_I, [_P, _P, _P, _P, _P, _I64, _I, _I, _P, _S]),

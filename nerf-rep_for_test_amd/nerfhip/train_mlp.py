@@ -1129,9 +1129,26 @@ class NerfMLPFn(torch.autograd.Function):
         else:
             d_hv, DF, D, d_enc = NerfMLPFn._backward_layers(DR, p, pk, bits, bits_v, dmax,
                                                             need_enc)
-        post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
-            "rgb_linear.weight", "rgb_linear.bias", None)
-        if heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
+        # T16: the view encoding rows and HV are adjacent forward rows (_FWD_ROWS),
+        # d_hv / d sigma / d rgb adjacent backward rows (HX): the views layer's
+        # encoding columns and the rgb head share ONE 147 x 160 tile,
+        # [d_hv; d sigma; d rgb] [enc; HV]^T, of which they are two blocks (the
+        # rest is discarded), instead of a 144 x 32 and a 16 x 128 tile: the
+        # batched launch's cost goes by tiles (a K step of a light tile costs
+        # about what a full one does, profiles/r5_wgrad_stream_studies/)
+        enc_rgb = heads_merged and t16 and ENC_RGB_TILE
+        if enc_rgb:
+            post[wb.add(rows_of(HX, 0, 147), V.rows(256, 416), (dmax[10:11], dmax[11:12]),
+                        (amax[10:11], amax[11:12]), with_bias=True, a_split=144)] = (
+                "views_enc_rgb", "views_enc_rgb_bias", None)
+        else:
+            post[wb.add(d_rgb, HV, dmax[11:12], amax[11:12], with_bias=True)] = (
+                "rgb_linear.weight", "rgb_linear.bias", None)
+        if enc_rgb:   # [G; g_alpha] = [d_hv; d sigma] h7^T (the encoding columns: above)
+            post[wb.add(rows_of(HX, 0, 129), V.rows(0, 256), (dmax[10:11], dmax[12:13]),
+                        amax[7:8], with_bias=True, a_split=128)] = (
+                "views_G", "views_GA_bias", None)
+        elif heads_merged:   # [G; g_alpha] = [d_hv; d sigma] [h7; enc]^T
             # d sigma (row 128) keeps its own FP16 split range: rows 128.. at
             # max |d sigma|, not at max |d hv| (a much larger d hv would flush it)
             post[wb.add(rows_of(HX, 0, 129), V, (dmax[10:11], dmax[12:13]),
@@ -1206,6 +1223,11 @@ class NerfMLPFn(torch.autograd.Function):
             grads[wname] = fix(gw) if fix is not None else gw
             if bname:
                 grads[bname] = gb
+        ER = erb = None
+        if "views_enc_rgb" in grads:   # the shared tile: vfg copies the rgb head out of it
+            ER, erb = grads.pop("views_enc_rgb"), grads.pop("views_enc_rgb_bias")
+            grads["rgb_linear.weight"] = torch.empty((3, 128), device=dev, dtype=f32)
+            grads["rgb_linear.bias"] = torch.empty((3,), device=dev, dtype=f32)
         if heads_merged:   # the views / feature / alpha gradients in one launch (below)
             GA, ba = grads.pop("views_G"), grads.pop("views_GA_bias")
             for n, shape in (("views_linears.0.weight", (128, 283)),
@@ -1220,6 +1242,9 @@ class NerfMLPFn(torch.autograd.Function):
                  ptr(Wv), ptr(grads["views_linears.0.weight"]), ptr(grads["feature_linear.weight"]),
                  ptr(grads["feature_linear.bias"]), ptr(grads["alpha_linear.weight"]),
                  ptr(grads["alpha_linear.bias"]), ptr(grads["views_linears.0.bias"]),
+                 *((None, 0, None, None, None) if ER is None else
+                   (ptr(ER), ER.stride(0), ptr(erb), ptr(grads["rgb_linear.weight"]),
+                    ptr(grads["rgb_linear.bias"]))),
                  _lib.stream_of(dev))
         elif v_h7:
             # feature = W_f h7 + b_f (NET:63) feeds the views layer (NET:64-65), so with
@@ -1236,6 +1261,9 @@ class NerfMLPFn(torch.autograd.Function):
             grads["feature_linear.bias"] = Wvf.t() @ sv
 
 
+# NERF_TRAIN_ENC_RGB_TILE=0: the views layer's encoding columns and the rgb head
+# in two tiles of their own (the A/B of the shared tile)
+ENC_RGB_TILE = _os.environ.get("NERF_TRAIN_ENC_RGB_TILE", "1") != "0"
 # NERF_TRAIN_SIDE_WGRAD=0: the weight gradients on the main stream, in line
 SIDE_WGRAD = _os.environ.get("NERF_TRAIN_SIDE_WGRAD", "1") != "0"
 _SIDE = {}

@@ -43,7 +43,7 @@ def test_ctypes_signatures_cover_header(lib_path):
     from nerfhip import _lib
     assert set(declared()) == set(_lib.SIGNATURES), set(declared()) ^ set(_lib.SIGNATURES)
     h = ctypes.CDLL(lib_path)
-    assert h.nerf_version() == 6
+    assert h.nerf_version() == 7
     h.nerf_last_error.restype = ctypes.c_char_p
     assert h.nerf_last_error() == b""
 

@@ -724,7 +724,7 @@ def test_views_feature_grads_kernel_matches_float64(dev):
         ("dba", (1,)), ("dbv", (128,)))}
     call("nerf_views_feature_grads", ptr(GA), ld, ptr(ba), ptr(Wf), ptr(bf), ptr(Wv),
          ptr(out["dWv"]), ptr(out["dWf"]), ptr(out["dbf"]), ptr(out["dWa"]), ptr(out["dba"]),
-         ptr(out["dbv"]), stream_of(dev))
+         ptr(out["dbv"]), None, 0, None, None, None, stream_of(dev))
     d = {k: v.double() for k, v in (("GA", GA), ("ba", ba), ("Wf", Wf), ("bf", bf), ("Wv", Wv))}
     Gh, s = d["GA"][:128, :256], d["ba"][:128]
     ref = {"dWv": torch.cat([Gh @ d["Wf"].t() + s[:, None] * d["bf"][None, :],
@@ -737,3 +737,37 @@ def test_views_feature_grads_kernel_matches_float64(dev):
     for k, r in ref.items():
         e = float((out[k].double() - r).abs().max())
         assert e <= 1e-6 * float(scale.get(k, 1.0)), (k, e)
+
+
+def test_views_feature_grads_from_the_shared_tile(dev):
+    """nerf_views_feature_grads with GE (the training backward's tile shared by
+    the views layer's encoding columns and the rgb head, [d_hv; d sigma; pad;
+    d rgb] [enc; HV]^T): the encoding columns of dW_views and the rgb head's
+    weight / bias gradients are copied out of it exactly; the rest as without."""
+    from nerfhip._lib import call, ptr, stream_of
+    g = torch.Generator(device=dev).manual_seed(22)
+    GA = torch.randn((129, 256), device=dev, generator=g)
+    ba = torch.randn((129,), device=dev, generator=g)
+    Wf = torch.randn((256, 256), device=dev, generator=g) * 0.1
+    bf = torch.randn((256,), device=dev, generator=g)
+    Wv = torch.randn((128, 283), device=dev, generator=g) * 0.1
+    ER = torch.randn((147, 170), device=dev, generator=g)
+    be = torch.randn((147,), device=dev, generator=g)
+    GA288 = torch.cat([GA, torch.cat([ER[:129, :27], torch.zeros((129, 5), device=dev)], 1)], 1)
+
+    def run(with_ge):
+        o = {k: torch.full(s, float("nan"), device=dev) for k, s in (
+            ("dWv", (128, 283)), ("dWf", (256, 256)), ("dbf", (256,)), ("dWa", (1, 256)),
+            ("dba", (1,)), ("dbv", (128,)), ("dWr", (3, 128)), ("dbr", (3,)))}
+        src = GA if with_ge else GA288.contiguous()
+        tail = ((ptr(ER), ER.stride(0), ptr(be), ptr(o["dWr"]), ptr(o["dbr"])) if with_ge
+                else (None, 0, None, None, None))
+        call("nerf_views_feature_grads", ptr(src), src.stride(0), ptr(ba), ptr(Wf), ptr(bf),
+             ptr(Wv), ptr(o["dWv"]), ptr(o["dWf"]), ptr(o["dbf"]), ptr(o["dWa"]), ptr(o["dba"]),
+             ptr(o["dbv"]), *tail, stream_of(dev))
+        return o
+    a, b = run(True), run(False)
+    for k in ("dWv", "dWf", "dbf", "dWa", "dba", "dbv"):
+        assert torch.equal(a[k], b[k]), k
+    assert torch.equal(a["dWv"][:, 256:], ER[:128, :27])
+    assert torch.equal(a["dWr"], ER[144:147, 32:160]) and torch.equal(a["dbr"], be[144:147])
