@@ -356,9 +356,11 @@ __device__ __forceinline__ void act_slices(f32x4 (&acc)[16], const Ring& R, int 
 }
 
 // ---------------------------------------------------------------------------
-// The training forward (TRAIN): the same kernel over the unfolded 73-slice
-// stream (the feature layer kept: its output and weights are the training
-// step's), which also writes every layer's output FP32 rows to HBM feature-
+// The training forward (TRAIN): the same kernel over the same 65-slice stream
+// (round 5: the feature layer folded into the views layer from the step's own
+// parameters by nerf_fold_views; the feature rows are never formed, the
+// views / feature weight gradients go through h7), which also writes every
+// layer's output FP32 rows to HBM feature-
 // major ([F][P], row stride ld: what the backward's weight gradients read),
 // the ReLU bits of h0..h7 and of the views layer in x3_layer_kernel's mask-bit
 // layout (its dgrad launches read them), and each output's max |.| (the weight
