@@ -81,13 +81,15 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["fp32", "f16x3"],
                     help="MLP arithmetic of the headline run: the 3-term FP16 split of the "
                          "FP32 operands on FP16 MFMA (default), or FP32 MFMA")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "dist-check"],
                     help="c2: lego 800x800 64c+128f (BASELINE configs[1], the headline); "
                          "c3: train step, 1024 rays/rank (configs[2]); "
                          "c4: c2 with ESS + ERT (configs[3], lego.yaml:96-99); "
                          "c5: the lego test set (the 25 packed views cycled, one per step, or "
                          "with --all-poses all 200 test poses; PSNR/SSIM over the --gt-path "
-                         "views from the sharded renders, configs[4])")
+                         "views from the sharded renders, configs[4]); dist-check: the "
+                         "launcher and the timed region's collectives alone (no render: "
+                         "tests/test_bench_launch.py runs it on the CPU over gloo)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 (ESS + ERT) sub-record of the default run")
     ap.add_argument("--checkpoint", default=None,
@@ -129,23 +131,34 @@ def main():
     if args.all_poses:
         POSE_STRIDE[0] = 1
 
+    # `python bench.py --gpus N` with no torchrun environment starts its own N
+    # ranks (one process per GPU) before this process touches the GPU
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
+
     import torch
     import torch.distributed as dist
-    from nerfhip import _lib
-    from nerfhip.render import NerfPipeline
-    from nerfhip.synthetic import make_occupancy_grid, make_params
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
-              file=sys.stderr)
     # NERF_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N > 1 path
     # (every collective, barrier and max-over-ranks of the timed region) on a
     # one-GPU box, ranks sharing the device; the driver's runs use RCCL ("nccl"),
     # one rank per GPU.
     backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+    err = launch_mismatch(args.gpus, world, backend, args.config)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr)
+        sys.exit(2)
+    if args.config == "dist-check":
+        return dist_check(args, world, rank, backend)
+
+    from nerfhip import _lib
+    from nerfhip.render import NerfPipeline
+    from nerfhip.synthetic import make_occupancy_grid, make_params
+
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -385,6 +398,133 @@ def main():
     if rank == 0:
         result["host"] = cpu
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def visible_gpus():
+    """ROCm devices this process may use, counted without initialising the GPU
+    (torch.cuda.device_count() on this image reads the device list only)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_mismatch(gpus, world, backend, config):
+    """Why this rank must not run, or None: --gpus has to equal the launch's
+    world size, and with RCCL every rank needs a GPU of its own. A mismatch
+    exits non-zero rather than timing fewer ranks than asked for."""
+    if world != gpus:
+        return (f"--gpus {gpus} but WORLD_SIZE {world}: launch N ranks with --gpus N "
+                f"(torchrun --nproc-per-node N, or python bench.py --gpus N alone)")
+    if backend == "nccl" and config != "dist-check":
+        n = visible_gpus()
+        if gpus > n:
+            return (f"--gpus {gpus} but {n} visible GPU(s): RCCL needs one GPU per rank "
+                    f"(NERF_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)")
+    return None
+
+
+def self_launch(args, argv=None):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: start N rank processes
+    of this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT set, one per visible GPU, and return the exit status for the
+    parent (the first failing rank's, else 0); rank 0 prints the JSON line. The
+    parent never touches the GPU: it counts devices, starts the ranks and waits.
+    Returns None when this process is itself a rank (WORLD_SIZE set) or N is 1."""
+    import signal
+    import socket
+    import subprocess
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+    err = launch_mismatch(args.gpus, args.gpus, backend, args.config)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = sys.argv[1:] if argv is None else argv
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, start_new_session=True))
+    # a SIGTERM to the launcher (a driver's time limit) takes the ranks down too
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    # one rank failed: the others would wait in a collective forever
+                    for q in pending:
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc
+
+
+def dist_check(args, world, rank, backend):
+    """--config dist-check: the multi-rank skeleton of every bench line without a
+    render -- process group, W untimed and K timed steps of one small all-reduce
+    bracketed by barriers, the elapsed time maxed over ranks, one JSON line on
+    rank 0 with n_gpus = the world size. gloo runs it on the CPU
+    (tests/test_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cpu")
+    if backend == "nccl":
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    x = torch.ones(1024, device=dev)
+
+    def step():
+        if world > 1:
+            dist.all_reduce(x)
+            x.div_(world)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "dist-check: all-reduce steps/s (launcher check, no render)",
+                          "value": args.steps / max(elapsed, 1e-9), "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / max(1, args.steps) * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                          "dtype": "fp32", "data": "synthetic",
+                          "config": {"workload": "dist-check", "backend": backend,
+                                     "ranks_pid": os.getpid()},
+                          "allreduce_ok": bool(torch.all(x == 1.0).item())}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -68,6 +68,15 @@ def unpack_maps(full, H, W, keys):
     return out
 
 
+def _collective(world):
+    """The gather runs whenever a process group is up -- at world 1 too, so the
+    RCCL all-gather and the reassembly are exercised by a one-GPU run
+    (tests/test_gpu_nccl.py: backend "nccl" at world 1, bit-equal to the
+    one-pass frame); with no group (a plain one-process render) the tile is the
+    frame."""
+    return world > 1 or (dist.is_available() and dist.is_initialized())
+
+
 def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
                          chunk_aligned=False):
     """render_band(p0, n) -> dict of flat maps for pixels [p0, p0+n) ({} when n
@@ -79,7 +88,7 @@ def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
     maps = render_band(p0, n) or {}
     keys = set(maps) if maps else set(MAP_ORDER)
     tile = pack_maps(maps, n, n_pad, device)
-    if world == 1:
+    if not _collective(world):
         full = tile
     else:
         full = torch.empty((world * n_pad, 12), device=device, dtype=torch.float32)
@@ -129,7 +138,7 @@ def render_frame_interleaved(render_chunks, H, W, rank, world, device, group=Non
     maps = render_chunks(mine) or {}
     keys = set(maps) if maps else set(MAP_ORDER)
     tile = pack_maps(maps, n, n_pad, device)
-    if world == 1:
+    if not _collective(world):
         full = tile[:H * W]
     else:
         full = torch.empty((world * n_pad, 12), device=device, dtype=torch.float32)

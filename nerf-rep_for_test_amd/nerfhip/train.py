@@ -426,6 +426,9 @@ class NerfTrainer:
         else:
             loss.backward(one)
         if group is not None:
+            for p in self.trained_parameters():
+                if p.grad is None:   # (a rank whose batch left a parameter untouched):
+                    p.grad = torch.zeros_like(p)   # every rank sends the same bucket
             allreduce_mean([p.grad for p in self.trained_parameters()], group)
         if self.adam != "hip":   # (HipAdam clamps the gradients itself, in place)
             torch.nn.utils.clip_grad_value_(self.trained_parameters(), self.clip_value)
