@@ -53,6 +53,7 @@ METRIC = "Mrays/s + ms/frame, lego 800x800 (64c+128f); PSNR vs ref"
 GT_STRIDE = 8          # tools/pack_lego.py: data/lego/test.npz = test frames 0, 8, ..., 192
 DEFAULT_CKPT = os.path.join(REPO, "checkpoints", "lego")
 GT_PATH = os.path.join(REPO, "data", "lego", "test.npz")
+TRAIN_PATH = os.path.join(REPO, "data", "lego", "train.npz")
 
 
 POSE_STRIDE = [GT_STRIDE]   # --all-poses: 1 (every one of the 200 test poses)
@@ -570,18 +571,36 @@ def make_frame_fn(pipe, H, W, rank, world, dev, ess_ert, perturb=False):
 
 def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmup=None,
                 emit=True):
-    """C3: NerfTrainer.step on 1024 random lego-camera pixels per rank (synthetic
-    targets), data parallel over ranks (weak scaling). emit=False: return the
+    """C3: NerfTrainer.step on 1024 random pixels of one random lego train view
+    per rank and step, their white-composited ground truth as the targets (the
+    reference's training batch: blender.py:60-84 images, lego.yaml:14 N_rays
+    1024, :19 no_batching; trainers/nerf.py:39-76 MSE coarse + fine), data
+    parallel over ranks (weak scaling). The 100 train views are decoded from
+    data/lego/train.npz (tools/pack_lego.py) and resident in HBM before timing;
+    without that file the step falls back to test-camera rays with uniform
+    random targets (same FLOPs; `data` says which). emit=False: return the
     record (the default bench run's "c3_train_step" sub-record) instead of
     printing it."""
     import torch
     import torch.distributed as dist
     from nerfhip.render import NerfPipeline
     from nerfhip.train import NerfTrainer, camera_rays_at
-    cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
     H = W = 800
-    focal = 0.5 * W / np.tan(0.5 * float(cams["camera_angle_x"]))
-    poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
+    images = None
+    if os.path.exists(TRAIN_PATH):
+        from nerfhip.evaluate import load_packed
+        imgs, tposes, focal, _ = load_packed(TRAIN_PATH)
+        assert imgs.shape[1:3] == (H, W), imgs.shape
+        images = torch.from_numpy(imgs).to(dev)
+        poses = torch.from_numpy(np.ascontiguousarray(tposes, dtype=np.float32)).to(dev)
+        del imgs
+        source = (f"{poses.shape[0]} lego train views (data/lego/train.npz, white-composited "
+                  f"ground truth as targets, {images.numel() * 4 / 2 ** 30:.2f} GiB resident)")
+    else:
+        cams = np.load(os.path.join(REPO, "tests", "golden", "lego_test_cameras.npz"))
+        focal = 0.5 * W / np.tan(0.5 * float(cams["camera_angle_x"]))
+        poses = torch.from_numpy(cams["poses"].astype(np.float32)).to(dev)
+        source = "lego test cameras with uniform random targets (data/lego/train.npz absent)"
     K = torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32,
                      device=dev)
     launch = "graph" if args.train_graph else args.train_launch
@@ -592,11 +611,16 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
     nrays = 1024
 
     def batch():
+        if images is None:
+            pix = torch.randint(0, H * W, (nrays,), device=dev, generator=gen)
+            view = torch.randint(0, poses.shape[0], (nrays,), device=dev, generator=gen)
+            ro, rd = camera_rays_at(poses, K, pix, view, W)
+            return ro, rd, torch.rand((nrays, 3), device=dev, generator=gen)
+        # one train view per step (no_batching), 1024 of its pixels
+        view = torch.randint(0, poses.shape[0], (1,), device=dev, generator=gen).expand(nrays)
         pix = torch.randint(0, H * W, (nrays,), device=dev, generator=gen)
-        view = torch.randint(0, poses.shape[0], (nrays,), device=dev, generator=gen)
         ro, rd = camera_rays_at(poses, K, pix, view, W)
-        target = torch.rand((nrays, 3), device=dev, generator=gen)
-        return ro, rd, target
+        return ro, rd, images[view, pix // W, pix % W].contiguous()
 
     n_steps = args.steps if steps is None else steps
     n_warm = max(3, args.warmup if warmup is None else warmup)   # the graph captures step 3
@@ -645,9 +669,14 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None,
         "dtype": DTYPES["f16x3"] if args.train_mlp == "x3" else "fp32",
-        "data": data + ", synthetic targets",
-        "config": {"workload": "lego train step: 1024 random pixels of the test cameras per "
-                               "rank, perturb 1, training-mode u, MSE coarse+fine, clip 40, Adam",
+        "data": data + "; rays and targets: " + source,
+        "config": {"workload": "lego train step: 1024 random pixels of one random train view "
+                               "per rank and step, their ground truth as targets, perturb 1, "
+                               "training-mode u, MSE coarse+fine, clip 40, Adam"
+                               if images is not None else
+                               "lego train step: 1024 random pixels of the test cameras per "
+                               "rank (train views absent), perturb 1, training-mode u, MSE "
+                               "coarse+fine, clip 40, Adam",
                    "baseline_config": "configs[2]", "N_rays": nrays, "N_samples": 64,
                    "N_importance": 128, "train_mlp": args.train_mlp,
                    "step_launch": ("one HIP graph replay per step (captured on the 3rd step)"

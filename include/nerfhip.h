@@ -480,6 +480,21 @@ int nerf_grid_update(const float* rays_d, const float* z, int64_t z_stride,
                      const float* raw, const float* weights, int64_t n, int S,
                      uint8_t* grid, int res, nerf_stream_t stream);
 
+/* VR:875-961 (_populate_occupancy_grid_kilonerf_method), in two launches
+ * around the MLP: nerf_grid_points writes the 27 sub-points of cells
+ * [cell0, cell0 + ncells) (cell f: x = f % res, y = (f % res^2) / res,
+ * z = f / res^2; sub-point 9 dz + 3 dy + dx at bbox_min + (x, y, z) * cell +
+ * (dx, dy, dz) / 2 * cell, torch's float32 op order) into pts[ncells * 27][3];
+ * the caller evaluates the coarse MLP on them (raw[ncells * 27][4]);
+ * nerf_grid_decide sets grid[cell_of[f]] (or, cell_of NULL, the cell's own
+ * [x][y][z] index) for every cell whose max relu(sigma) exceeds threshold
+ * (0.01 in the reference). bbox_min / cell_size: host arrays. The caller
+ * zeroes the grid first (VR:894). */
+int nerf_grid_points(int64_t cell0, int64_t ncells, int res, const float bbox_min[3],
+                     const float cell_size[3], float* pts, nerf_stream_t stream);
+int nerf_grid_decide(const float* raw, int64_t cell0, int64_t ncells, int res, float threshold,
+                     const int32_t* cell_of, uint8_t* grid, nerf_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * 2. kilonerf_cuda op contract (cuda/pybind.cu:13-38)
  * ------------------------------------------------------------------------- */

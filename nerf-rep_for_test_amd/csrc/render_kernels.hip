@@ -1181,6 +1181,88 @@ int nerf_add_sigma_noise(const float* raw, const float* noise, int64_t count, fl
   return check_launch("add_sigma_noise_kernel");
 }
 
+// ---------------------------------------------------------------------------
+// VR:875-961 _populate_occupancy_grid_kilonerf_method: the 27 sub-points of
+// cells [cell0, cell0 + ncells) in the method's flat order (cell f: z = f / res^2,
+// y = (f % res^2) / res, x = f % res, :903-906), sub-point s = 9 dz + 3 dy + dx
+// (:913-920), point = (bbox_min + (x, y, z) * cell) + (d / 2) * cell, every
+// product and sum rounded as torch's separate float32 ops (:908-918).
+__global__ __launch_bounds__(256) void grid_points_kernel(int64_t cell0, int64_t count, int res,
+                                                          float bx, float by, float bz, float cx,
+                                                          float cy, float cz,
+                                                          float* __restrict__ pts) {
+  const int64_t rr = (int64_t)res * res;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = cell0 + i / 27;
+    const int s = (int)(i % 27);
+    const float x = (float)(f % res), y = (float)((f % rr) / res), z = (float)(f / rr);
+    const float ox = (float)(s % 3) / 2.0f, oy = (float)((s / 3) % 3) / 2.0f,
+                oz = (float)(s / 9) / 2.0f;
+    const float mx = __fadd_rn(bx, __fmul_rn(x, cx)), my = __fadd_rn(by, __fmul_rn(y, cy)),
+                mz = __fadd_rn(bz, __fmul_rn(z, cz));
+    pts[3 * i + 0] = __fadd_rn(mx, __fmul_rn(ox, cx));
+    pts[3 * i + 1] = __fadd_rn(my, __fmul_rn(oy, cy));
+    pts[3 * i + 2] = __fadd_rn(mz, __fmul_rn(oz, cz));
+  }
+}
+
+// VR:937-953: per cell the largest relu(sigma) of its 27 points (torch's max
+// propagates NaN, and NaN > thr is false), > thr marks the cell -- at grid
+// index cell_of[f] (the reference's list(set(...)) order, built on the host)
+// or, with cell_of NULL, at the cell's own [x][y][z] index.
+__global__ __launch_bounds__(256) void grid_decide_kernel(const float4* __restrict__ raw,
+                                                          int64_t cell0, int64_t ncells, int res,
+                                                          float thr,
+                                                          const int32_t* __restrict__ cell_of,
+                                                          uint8_t* __restrict__ grid) {
+  const int64_t rr = (int64_t)res * res;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncells;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    float m = 0.0f;
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      const float v = raw[c * 27 + k].w;
+      nan |= v != v;
+      m = fmaxf(m, v);   // relu then max: max(0, v_0, ..., v_26)
+    }
+    if (!nan && m > thr) {
+      const int64_t f = cell0 + c;
+      const int64_t own = ((f % res) * res + (f % rr) / res) * res + f / rr;
+      grid[cell_of ? (int64_t)cell_of[f] : own] = 1;
+    }
+  }
+}
+
+int nerf_grid_points(int64_t cell0, int64_t ncells, int res, const float bbox_min[3],
+                     const float cell_size[3], float* pts, nerf_stream_t stream) {
+  NERF_REQUIRE(pts && bbox_min && cell_size, "nerf_grid_points: null pointer");
+  NERF_REQUIRE(res >= 1 && res <= 1024 && cell0 >= 0 && ncells >= 0 &&
+                   cell0 + ncells <= (int64_t)res * res * res,
+               "nerf_grid_points: bad cell range");
+  if (ncells == 0) return 0;
+  const int64_t count = ncells * 27;
+  const int64_t blocks = std::min<int64_t>(cdiv(count, 256), 256 * 64);
+  hipLaunchKernelGGL(grid_points_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     as_stream(stream), cell0, count, res, bbox_min[0], bbox_min[1], bbox_min[2],
+                     cell_size[0], cell_size[1], cell_size[2], pts);
+  return check_launch("grid_points_kernel");
+}
+
+int nerf_grid_decide(const float* raw, int64_t cell0, int64_t ncells, int res, float threshold,
+                     const int32_t* cell_of, uint8_t* grid, nerf_stream_t stream) {
+  NERF_REQUIRE(raw && grid, "nerf_grid_decide: null pointer");
+  NERF_REQUIRE(res >= 1 && res <= 1024 && cell0 >= 0 && ncells >= 0 &&
+                   cell0 + ncells <= (int64_t)res * res * res,
+               "nerf_grid_decide: bad cell range");
+  if (ncells == 0) return 0;
+  const int64_t blocks = std::min<int64_t>(cdiv(ncells, 256), 256 * 64);
+  hipLaunchKernelGGL(grid_decide_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     (const float4*)raw, cell0, ncells, res, threshold, cell_of, grid);
+  return check_launch("grid_decide_kernel");
+}
+
 int nerf_composite(const float* raw, const float* z, int64_t z_stride, const float* rays_d,
                    int64_t n, int S, int white_bkgd, float* rgb, float* disp, float* acc,
                    float* depth, float* weights, nerf_stream_t stream) {

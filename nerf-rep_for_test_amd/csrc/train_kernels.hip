@@ -591,7 +591,9 @@ __global__ __launch_bounds__(256) void views_feature_grads_kernel(
   const int tile = views ? blk : blk - kVfTilesV;
   const int m0 = 32 * (tile >> 3), n0 = 32 * (tile & 7);
   const int K = views ? 256 : 128;
+  // 67.6 KB: gfx950's 160 KiB per workgroup (the Makefile builds for gfx950 only)
   __shared__ float As[256][33], Bs[256][33];   // As[k][m], Bs[k][n]
+  static_assert(sizeof(As) + sizeof(Bs) <= 160 * 1024, "gfx950 LDS per workgroup");
   const int tm = t >> 4, tn = t & 15;          // outputs (m0 + 2 tm + a, n0 + 2 tn + b)
   if (views) {
     // A(m, k) = GA[m][k], B(k, n) = W_f[n][k] (k contiguous): 32 rows x 256 k each

@@ -61,6 +61,8 @@ SIGNATURES = {
                                              _P, _S]),
     "nerf_composite": (_I, [_P, _P, _I64, _P, _I64, _I, _I, _P, _P, _P, _P, _P, _S]),
     "nerf_add_sigma_noise": (_I, [_P, _P, _I64, _P, _S]),
+    "nerf_grid_points": (_I, [_I64, _I64, _I, C.POINTER(_F), C.POINTER(_F), _P, _S]),
+    "nerf_grid_decide": (_I, [_P, _I64, _I64, _I, _F, _P, _P, _S]),
     "nerf_fold_views": (_I, [_P, _I, _S]),
     "nerf_linear_fm": (_I, [_P, _I64, _P, _P, _I64, _I, _I64, _I, _I, _P, _I64, _I64, _S]),
     "nerf_composite_ert_workspace": (_SZ, [_I64, _I]),

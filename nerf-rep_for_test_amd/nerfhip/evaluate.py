@@ -11,6 +11,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -47,19 +49,33 @@ def decode_png(buf):
         np.float32(255.0)
 
 
-def load_packed(path, H=None, W=None, indices=None):
+def load_packed(path, H=None, W=None, indices=None, workers=None):
     """Views packed by tools/pack_lego.py as the reference's dataset yields them
     (blender.py:38-84): white-composited RGB [N,H,W,3] float32, poses [N,4,4],
     focal (0.5 W / tan(0.5 camera_angle_x), blender.py:41-42) and the json frame
-    indices."""
+    indices. The views are decoded and composited on a thread pool (PIL's
+    decoder and numpy release the GIL; ~75 ms of CPU per 800x800 view), each
+    into its slot of one preallocated array."""
+    from concurrent.futures import ThreadPoolExecutor
     z = np.load(path)
     offs = z["png_offsets"]
-    idx = range(len(offs) - 1) if indices is None else indices
-    imgs = []
-    for i in idx:
-        img = composite_white(decode_png(z["png_bytes"][offs[i]:offs[i + 1]]))
-        imgs.append(resize_bilinear(img, H or img.shape[0], W or img.shape[1]))
-    imgs = np.stack(imgs)
+    buf = z["png_bytes"]
+    idx = list(range(len(offs) - 1) if indices is None else indices)
+
+    def one(i):
+        img = composite_white(decode_png(buf[offs[i]:offs[i + 1]]))
+        return resize_bilinear(img, H or img.shape[0], W or img.shape[1])
+
+    first = one(idx[0]) if idx else np.zeros((H or 0, W or 0, 3), np.float32)
+    imgs = np.empty((len(idx),) + first.shape, np.float32)
+    if idx:
+        imgs[0] = first
+
+        def put(k):
+            imgs[k] = one(idx[k])
+        n = workers or min(16, os.cpu_count() or 1, len(idx))
+        with ThreadPoolExecutor(max(1, n)) as ex:
+            list(ex.map(put, range(1, len(idx))))
     focal = 0.5 * imgs.shape[2] / np.tan(0.5 * float(z["camera_angle_x"]))
     return imgs, z["poses"][list(idx)], float(focal), z["frames"][list(idx)]
 

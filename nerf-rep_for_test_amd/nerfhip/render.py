@@ -14,6 +14,9 @@ the kernels see the reference's exact float32 values.
 """
 from __future__ import annotations
 
+import ctypes
+
+import numpy as np
 import torch
 
 from . import _lib
@@ -40,6 +43,32 @@ def reference_draws(n, S, NI, perturb, draw_u, device):
     fine-sampling u [m, NI]. Returns (t_rand [n, S] | None, u [n, NI] | None), so
     a whole-frame pass consumes the same random stream as the chunk loop."""
     return reference_draws_noise(n, S, NI, perturb, draw_u, device, 0.0)[:2]
+
+
+_CELL_ORDER = {}
+
+
+def reference_cell_order(res, device=None, batch=512):
+    """VR:896-953's assignment of a batch's decisions to cells: the batch of
+    cells [b, b + 512) (flat order f: x = f % res, y = (f % res^2) // res,
+    z = f // res^2; each listed 27 times, once per sub-point, VR:903-922) gives
+    its k-th decision to the k-th element of ``list(set(batch_indices))``.
+    Returns int32 [res^3]: the [x][y][z] grid index that cell f's decision
+    lands on (cached per resolution). CPython's iteration order of a set of
+    small-int tuples is deterministic (tuple hashes of ints are not salted);
+    building the set from the unique tuples in first-occurrence order gives the
+    same table as with the 27 repeats (asserted by tests/test_kilonerf_grid.py)."""
+    key = (res, batch)
+    if key not in _CELL_ORDER:
+        out = np.empty(res ** 3, np.int32)
+        rr = res * res
+        for b in range(0, res ** 3, batch):
+            cells = [(f % res, (f % rr) // res, f // rr) for f in range(b, min(b + batch, res ** 3))]
+            order = list(set(cells))
+            out[b:b + len(order)] = [(x * res + y) * res + z for x, y, z in order]
+        _CELL_ORDER[key] = out
+    t = torch.from_numpy(_CELL_ORDER[key])
+    return t.to(device) if device is not None else t
 
 
 def reference_draws_noise(n, S, NI, perturb, draw_u, device, noise_std):
@@ -114,6 +143,8 @@ class NerfPipeline:
         self.timer = None         # list -> (start event, end event, samples, bytes) per MLP launch
         self.stage_timer = None   # list -> (kernel, start event, end event, algorithmic bytes)
         self.capture_zall = None  # list -> the merged fine depths [m, S+NI] of every pass (tests)
+        self.capture_coarse = None   # list -> (coarse depths [m, S], coarse weights [m, S])
+                                     # of every pass: what the fine sampling read (tests)
         self._replaying = False   # replays of foreign update chunks: not in ert_stats
         self.replayed_chunks = 0  # foreign update chunks replayed (multi-GPU C4 overhead)
         self._updates_on = True   # render_chunks switches the grid self-update off for blocks
@@ -143,6 +174,46 @@ class NerfPipeline:
         g = torch.as_tensor(grid)
         self.grid_res = int(g.shape[0])
         self.grid = g.to(device=self.device, dtype=torch.uint8).contiguous().view(-1)
+
+    def populate_grid_kilonerf(self, res=None, bbox_min=(-2.0, -2.0, -2.0),
+                               bbox_max=(2.0, 2.0, 2.0), threshold=0.01, reference_order=True,
+                               cells_per_pass=1 << 18):
+        """The reference's density-driven occupancy grid (VR:875-961,
+        ``_populate_occupancy_grid_kilonerf_method``) on the HIP path: the 27
+        sub-points of every cell (nerf_grid_points), the coarse network's density
+        there (the fused MLP of this pipeline's precision: points as rays with a
+        zero depth; sigma does not depend on the view input, network.py:59-61),
+        and a cell marked where the largest relu(sigma) exceeds ``threshold``
+        (nerf_grid_decide). ``reference_order``: each 512-cell batch's decisions
+        land on the cells in CPython's iteration order of the batch's
+        ``set`` of (x, y, z) tuples, as the reference writes them (VR:950-953,
+        reference_cell_order); False: every cell's own decision at its own
+        place. Replaces the pipeline's grid and returns it ([res^3] uint8)."""
+        res = int(res or self.grid_res or 128)
+        bmin = np.asarray(bbox_min, np.float32)
+        cell = (np.asarray(bbox_max, np.float32) - bmin) / np.float32(res)   # VR:889-890
+        dev = self.device
+        st = _lib.stream_of(dev)
+        grid = torch.zeros(res ** 3, device=dev, dtype=torch.uint8)       # VR:894
+        cell_of = reference_cell_order(res, dev) if reference_order else None
+        cf = (ctypes.c_float * 3)
+        bm, cs = cf(*bmin.tolist()), cf(*cell.tolist())
+        z0 = torch.zeros(1, device=dev, dtype=torch.float32)
+        dirs = None
+        total = res ** 3
+        for c0 in range(0, total, cells_per_pass):
+            nc = min(cells_per_pass, total - c0)
+            m = nc * 27
+            pts = torch.empty((m, 3), device=dev, dtype=torch.float32)
+            call("nerf_grid_points", c0, nc, res, bm, cs, ptr(pts), st)
+            if dirs is None or dirs.shape[0] < m:
+                dirs = torch.tensor([0.0, 0.0, 1.0], device=dev).expand(m, 3).contiguous()
+            raw = self.mlp(self.coarse, pts, dirs[:m], z0, 0, m, 1)
+            call("nerf_grid_decide", ptr(raw), c0, nc, res, float(threshold), ptr(cell_of),
+                 ptr(grid), st)
+            del pts, raw
+        self.set_grid(grid.view(res, res, res))
+        return self.grid
 
     # ------------------------------------------------------------------ stages
     # algorithmic MACs of one NeRF MLP evaluation (NET:49-74): 63*256 + 4*256^2
@@ -279,7 +350,8 @@ class NerfPipeline:
             counter0 = self.grid_update_counter
             ro, rd = rays_o[p:p + m], rays_d[p:p + m]
             tr = None if t_rand is None else t_rand[p:p + m]
-            nz_c, nz_f = (None, None) if noise is None else (noise[0][p:p + m], noise[1][p:p + m])
+            nz_c, nz_f = (None, None) if noise is None else tuple(
+                None if x is None else x[p:p + m] for x in noise)
             if self.enable_ess:
                 if self.grid is None:
                     raise _lib.NerfHipError("ESS enabled but no occupancy grid set")
@@ -296,6 +368,9 @@ class NerfPipeline:
                 z, zs = self.z_base, 0                     # one shared row (expand)
             raw = self._pass_mlp(self.coarse, ro, rd, z, zs, m, S, compact=noise is None)
             w = self.composite(raw, z, zs, rd, m, S, outputs["coarse"], off + p, noise=nz_c)
+            if self.capture_coarse is not None:
+                self.capture_coarse.append(((z if zs else z.expand(m, S)).clone(),
+                                            w.reshape(m, S).clone()))
             self._grid_updates(0, counter0, rd, z, zs, raw, w, m, S)
             if NI > 0:
                 zall = torch.empty((m, S + NI), device=dev, dtype=torch.float32)
@@ -470,7 +545,7 @@ class NerfPipeline:
         return [c for c in range(total)
                 if any((cf + per * c + k) % self.grid_update_interval == 0 for k in range(per))]
 
-    def render_chunks(self, H, W, pose, K, chunks, t_rand=None):
+    def render_chunks(self, H, W, pose, K, chunks, t_rand=None, noise=None):
         """The reference chunks `chunks` (ascending ids of 2048 consecutive
         pixels, VR:147) of a frame whose other chunks other ranks render
         concurrently (dist.render_frame_interleaved: chunk c on rank c mod P),
@@ -489,7 +564,9 @@ class NerfPipeline:
         so every rank leaves the frame with the sequential loop's grid and
         counter. Cost: one extra chunk per foreign update chunk (2 per 500
         ERT calls). t_rand: the frame's perturb draws [H * W, N_samples] (every
-        rank holds the same; a chunk reads its own rows)."""
+        rank holds the same; a chunk reads its own rows); noise: the frame's
+        density noise (coarse [H * W, S], fine [H * W, S + NI], raw_noise_std > 0,
+        reference_draws_noise), read by rows the same way."""
         total = -(-H * W // REF_CHUNK)
         chunks = [int(c) for c in chunks]
         if chunks != sorted(set(chunks)) or (chunks and not 0 <= chunks[0] <= chunks[-1] < total):
@@ -506,15 +583,17 @@ class NerfPipeline:
             idx = torch.cat([torch.arange(c * REF_CHUNK, c * REF_CHUNK + min(
                 REF_CHUNK, H * W - c * REF_CHUNK), device=self.device) for c in cs])
             tr = None if t_rand is None else t_rand.index_select(0, idx)
-            return rays_o.index_select(0, idx), rays_d.index_select(0, idx), tr
+            nz = None if noise is None else tuple(
+                None if x is None else x.index_select(0, idx) for x in noise)
+            return rays_o.index_select(0, idx), rays_d.index_select(0, idx), tr, nz
 
         def block(i0, i1):           # own chunks chunks[i0:i1] as one block, no updates inside
             if i1 <= i0:
                 return
-            ro, rd, tr = rows(chunks[i0:i1])
+            ro, rd, tr, nz = rows(chunks[i0:i1])
             self._updates_on = False
             try:
-                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i0])
+                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i0], noise=nz)
             finally:
                 self._updates_on = True
 
@@ -531,12 +610,12 @@ class NerfPipeline:
             block(i, j)
             i = j
             self.grid_update_counter = cf + per * u
-            ro, rd, tr = rows([u])
+            ro, rd, tr, nz = rows([u])
             if i < len(chunks) and chunks[i] == u:
-                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i])
+                self.render_rays(ro, rd, t_rand=tr, outputs=outputs, off=offs[i], noise=nz)
                 i += 1
             else:
-                self._replay(lambda: self.render_rays(ro, rd, t_rand=tr))
+                self._replay(lambda: self.render_rays(ro, rd, t_rand=tr, noise=nz))
         block(i, len(chunks))
         self.grid_update_counter = cf + per * total
         return maps_dict(outputs) if chunks else {}

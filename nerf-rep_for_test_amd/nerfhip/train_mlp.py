@@ -1318,8 +1318,10 @@ def _join_side(side, wb, grads, stats, params, dev):
     """After the side-stream weight gradients: every buffer they read stays
     allocated until they are done (record_stream), the gradients are handed to
     the main stream, which waits for them at the end of the backward pass (an
-    engine callback) -- or at once when a parameter already holds a gradient
-    (AccumulateGrad then adds into it right away)."""
+    engine callback) -- or at once when anything reads them on the main stream
+    sooner: a parameter that already holds a gradient (AccumulateGrad adds into
+    it right away), grad mode (create_graph: AccumulateGrad copies), or a
+    tensor / post-accumulate-grad hook on a parameter."""
     main = torch.cuda.current_stream(dev)
 
     def keep(t):
@@ -1339,7 +1341,13 @@ def _join_side(side, wb, grads, stats, params, dev):
         g.record_stream(main)
     ev = torch.cuda.Event()
     ev.record(side)
-    if any(q.grad is not None for q in params):
+    # the main stream must wait at once whenever something on it may read a
+    # gradient before the pass ends: AccumulateGrad adding into an existing
+    # .grad, or copying the gradient in grad mode (create_graph), and tensor /
+    # post-accumulate hooks, which the engine runs on the main stream
+    hooked = any(getattr(q, "_backward_hooks", None) or
+                 getattr(q, "_post_accumulate_grad_hooks", None) for q in params)
+    if torch.is_grad_enabled() or hooked or any(q.grad is not None for q in params):
         main.wait_event(ev)
     else:
         torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_event(ev))

@@ -102,6 +102,24 @@ class Renderer:
         self.pipeline.ess_skip_threshold = self.ess_skip_threshold
         self.pipeline.grid_update_interval = self.grid_update_interval
 
+    def _populate_occupancy_grid_kilonerf_method(self):
+        """Reference VR:875-961: the Renderer's grid rebuilt from the coarse
+        network's density -- the largest relu(sigma) of 3 x 3 x 3 sub-points per
+        cell above 0.01 -- at its resolution over the scene box, on the HIP path
+        (NerfPipeline.populate_grid_kilonerf: the sub-points and the decision as
+        two small kernels around one fused MLP launch per pass). Each 512-cell
+        batch's decisions land on the cells in the order the reference writes
+        them (VR:950-953, list(set(...))). Unlike the reference, which hands the
+        network its xyz encoding alone and so raises in NeRF.forward
+        (network.py:49-51), it runs: the density does not depend on the view
+        input. Only with ESS on (VR:880-881)."""
+        if not self.enable_ess or self.coarse_model is None:
+            return
+        self._sync_weights()
+        self.pipeline.populate_grid_kilonerf(
+            self.occupancy_grid_resolution, self.scene_bbox_min.tolist(),
+            self.scene_bbox_max.tolist(), threshold=0.01)
+
     @property
     def occupancy_grid(self):
         g = self.pipeline.grid

@@ -510,3 +510,56 @@ def render(H, W, pose, K, params, cfg: RenderConfig, t_rand=None, u_fine=None,
     if return_zall and zalls:
         res["zall"] = np.concatenate(zalls, 0)
     return res, counter
+
+
+# ----------------------------------------------------------------------------
+# density-driven occupancy grid (VR:875-961)
+# ----------------------------------------------------------------------------
+def grid_points(res, bbox_min=(-2.0, -2.0, -2.0), bbox_max=(2.0, 2.0, 2.0)):
+    """VR:885-922: the 27 sub-points of every cell, [res^3, 27, 3] float32, in
+    the method's flat cell order (f: x = f % res, y = (f % res^2) // res,
+    z = f // res^2, VR:903-906) and sub-point order (dz, dy, dx, VR:913-915);
+    point = (min + (x, y, z) * cell) + ((dx, dy, dz) / 2) * cell, one float32
+    rounding per torch op (VR:908, :918-919)."""
+    bmin = np.asarray(bbox_min, F32)
+    cell = ((np.asarray(bbox_max, F32) - bmin) / F32(res)).astype(F32)      # VR:889-890
+    f = np.arange(res ** 3)
+    xyz = np.stack([f % res, (f % (res * res)) // res, f // (res * res)], -1).astype(F32)
+    cmin = (bmin + (xyz * cell).astype(F32)).astype(F32)
+    d = np.arange(27)
+    off = (np.stack([d % 3, (d // 3) % 3, d // 9], -1).astype(F32) / F32(2.0)).astype(F32)
+    return (cmin[:, None, :] + (off[None] * cell).astype(F32)).astype(F32)
+
+
+def reference_cell_order(res, batch=512):
+    """VR:950-953: the 512-cell batch's k-th decision lands on the k-th cell of
+    list(set(batch_indices)) (each (x, y, z) listed 27 times, VR:922); returns
+    the [x][y][z] index per flat cell (int64)."""
+    out = np.empty(res ** 3, np.int64)
+    rr = res * res
+    for b in range(0, res ** 3, batch):
+        idx = []
+        for f in range(b, min(b + batch, res ** 3)):
+            idx += [(f % res, (f % rr) // res, f // rr)] * 27
+        order = list(set(idx))
+        out[b:b + len(order)] = [(x * res + y) * res + z for x, y, z in order]
+    return out
+
+
+def populate_grid_kilonerf(params, res, threshold=0.01, reference_order=True, prefix="model"):
+    """VR:875-961 with the coarse network (sigma does not depend on the view
+    input, NET:59-61, so any direction serves; the reference itself cannot run
+    the method as written, see tests/golden/make_kilonerf_grid.py): the largest
+    relu(sigma) of each cell's 27 points, > threshold, written through the
+    reference's cell order. Returns (grid bool [res, res, res], cell max
+    density float32 [res^3])."""
+    pts = grid_points(res)
+    dirs = np.tile(np.array([[0.0, 0.0, 1.0]], F32), (pts.shape[0], 1))
+    raw = query_network(pts, dirs, params, prefix)
+    dens = np.maximum(raw[..., 3], F32(0.0)).max(1)
+    grid = np.zeros(res ** 3, bool)
+    dest = reference_cell_order(res) if reference_order else \
+        (np.arange(res ** 3) % res * res + (np.arange(res ** 3) % (res * res)) // res) * res \
+        + np.arange(res ** 3) // (res * res)
+    grid[dest[dens > F32(threshold)]] = True
+    return grid.reshape(res, res, res), dens

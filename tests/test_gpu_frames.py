@@ -122,7 +122,7 @@ def _pix_err(got, ref, kind):
     return e, tol
 
 
-def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
+def _tail_given_reference_depths(name, prec, z, zh, tail_pix, zall_hip, coarse_hip, fine):
     """Every tail pixel (beyond tolerance and beyond 4x the reference's own
     spread) re-rendered on the reference's OWN fine depths.
 
@@ -153,6 +153,7 @@ def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
     rep = {"tail_captured": int(cap.sum()), "tail_uncaptured": int((~cap).sum()),
            "tail_uncaptured_pixels": tail_pix[~cap][:20].tolist(),
            "tail_oracle_hash_mismatch": 0, "tail_given_ref_depths_max_err": {},
+           "tail_causal_coarse_z_equal": True, "tail_causal_mismatch": 0,
            "tail_given_ref_depths_max_ratio": 0.0}
     if len(T) == 0:
         return rep
@@ -162,6 +163,7 @@ def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
     zf = O.sample_fine(mids, wc[:, 1:-1], O.linspace_f32(0.0, 1.0, 128))
     zall = np.ascontiguousarray(np.sort(np.concatenate([zc, zf], -1), -1), np.float32)
     rep["tail_oracle_hash_mismatch"] = int((row_hash(zall) != zh["zall_hash"][T]).sum())
+    rep.update(_tail_causal_chain(T, zc, wc, zall_hip, coarse_hip, zh, fine))
     dev = torch.device("cuda:0")
     ert = bool(z["ert"])
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128, enable_ert=ert,
@@ -235,6 +237,45 @@ def _tail_given_reference_depths(name, prec, z, zh, tail_pix):
     return rep
 
 
+def _tail_causal_chain(T, zc_ref, wc_ref, zall_hip, coarse_hip, zh, fine):
+    """Why a tail pixel's fine depths differ from the reference's (verdict r5):
+    HIP's coarse depths of the pixel are the reference's bit for bit, its coarse
+    weights differ by rounding only (reported: the largest |w_hip - w_ref|
+    relative to the ray's largest weight), and the oracle's sample_fine + merge
+    (VR:239-268, :183) of HIP's OWN weights reproduces HIP's own fine row
+    (tail_causal_mismatch == 0) -- so every other fine depth HIP draws comes from
+    the fine sampling's conditioning on rounding-level weight noise, not from a
+    defect of the HIP sampler or MLP. Every captured tail pixel is checked; the
+    ones beyond 1e-4 on fine rgb are listed."""
+    from oracle import nerf_oracle as O
+    idx = torch.from_numpy(T).to(coarse_hip[0].device)
+    zc_h = coarse_hip[0][idx].cpu().numpy()
+    wc_h = coarse_hip[1][idx].cpu().numpy()
+    mids = (np.float32(0.5) * (zc_h[:, 1:] + zc_h[:, :-1])).astype(np.float32)
+    zf = O.sample_fine(mids, wc_h[:, 1:-1], O.linspace_f32(0.0, 1.0, 128))
+    zall_o = np.ascontiguousarray(np.sort(np.concatenate([zc_h, zf], -1), -1), np.float32)
+    h_hip = row_hash(np.ascontiguousarray(zall_hip[T]))
+    dw = np.abs(wc_h.astype(np.float64) - wc_ref.astype(np.float64))
+    scale = np.maximum(np.abs(wc_ref).max(-1), 1e-30)[:, None]
+    rel = (dw / scale).max(-1)
+    other = h_hip != zh["zall_hash"][T]
+    e_rgb = fine["rgb"][0][T]
+    big = np.flatnonzero(e_rgb > 1e-4)
+    return {"tail_causal_coarse_z_equal": bool(np.array_equal(zc_h, zc_ref)),
+            "tail_causal_mismatch": int((row_hash(zall_o) != h_hip).sum()),
+            "tail_causal_rows_other_than_ref": int(other.sum()),
+            "tail_causal_w_max_abs_diff": float(dw.max()) if len(dw) else 0.0,
+            "tail_causal_w_max_rel_diff": float(rel.max()) if len(rel) else 0.0,
+            "tail_causal_w_max_rel_diff_other_rows": float(rel[other].max()) if other.any()
+            else 0.0,
+            "tail_causal_fine_rgb_over_1e-4": [
+                {"pixel": int(T[i]), "fine_rgb_err": float(e_rgb[i]),
+                 "fine_rows_differ_from_ref": bool(other[i]),
+                 "coarse_w_max_abs_diff": float(dw[i].max()),
+                 "coarse_w_max_rel_diff": float(rel[i])}
+                for i in big[np.argsort(-e_rgb[big])][:20]]}
+
+
 ERT_FLIP_REL = 1e-4
 
 
@@ -273,7 +314,8 @@ def _ert_threshold_flips(z, pix, zall, thr):
     return out
 
 
-def _check(name, prec, z, got, zall_hip, extra=None):
+def _check(name, prec, z, got, cap, extra=None):
+    zall_hip, coarse_hip = cap
     H, W = int(z["H"]), int(z["W"])
     n = H * W
     zh = _zh(name)
@@ -368,7 +410,8 @@ def _check(name, prec, z, got, zall_hip, extra=None):
                 "depth_hip": float(got["depth_map"].reshape(n)[i]),
                 **{f"{k}_err": float(e[i]) for k, (e, _) in fine.items()}}
                for i in np.flatnonzero(unexpl)[:20]],
-           **_tail_given_reference_depths(name, prec, z, zh, np.flatnonzero(tail)),
+           **_tail_given_reference_depths(name, prec, z, zh, np.flatnonzero(tail),
+                                          zall_hip, coarse_hip, fine),
            "psnr_hip_vs_ref": float("inf") if mse == 0 else -10 * np.log10(mse),
            "reference_cpu_seconds": float(z["cpu_seconds"])}
     if extra:
@@ -390,6 +433,9 @@ def _check(name, prec, z, got, zall_hip, extra=None):
     # the whole tail, on the reference's own depths (verdict r4 item 1)
     assert rep["tail_uncaptured"] == 0, rep
     assert rep["tail_oracle_hash_mismatch"] == 0, rep
+    # HIP's different fine rows come from its coarse weights' rounding alone
+    assert rep["tail_causal_coarse_z_equal"], rep
+    assert rep["tail_causal_mismatch"] == 0, rep
     assert rep["tail_given_ref_depths_max_ratio"] <= 1.0, rep
     assert rep["tail_given_ref_depths_ert_threshold_flips"] <= 5, rep
     assert rep["psnr_hip_vs_ref"] >= 60.0, rep
@@ -403,15 +449,20 @@ def test_c2_frame0_vs_reference(dev, prec):
     pipe = NerfPipeline(dev, N_samples=64, N_importance=128, mlp_precision=prec)
     pipe.load_checkpoint(CKPT_DIR)
     pipe.capture_zall = []
+    pipe.capture_coarse = []
     res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     _check("r0_c2_frame0", prec, z, {k: v.cpu().numpy() for k, v in res.items()},
            _zall(pipe))
 
 
 def _zall(pipe):
+    """(HIP's fine rows of every ray [n, 192], (coarse depths, coarse weights)
+    [n, 64] each on the device: what its fine sampling read)."""
     zall = torch.cat(pipe.capture_zall).cpu().numpy()
-    pipe.capture_zall = None
-    return zall
+    coarse = (torch.cat([c[0] for c in pipe.capture_coarse]),
+              torch.cat([c[1] for c in pipe.capture_coarse]))
+    pipe.capture_zall = pipe.capture_coarse = None
+    return zall, coarse
 
 
 @pytest.mark.parametrize("prec", ["f16x3", "fp32"])
@@ -444,6 +495,7 @@ def test_c2_perturbed_frame_through_plugin(dev, prec):
     batch = {"H": int(z["H"]), "W": int(z["W"]), "pose": torch.from_numpy(z["pose"])[None],
              "intrinsics": torch.from_numpy(z["K"])[None]}
     rend.pipeline.capture_zall = []
+    rend.pipeline.capture_coarse = []
     torch.rand = rand
     try:
         with torch.no_grad():
@@ -472,6 +524,7 @@ def test_c4_frame16_vs_reference(dev, prec):
     pipe.set_grid(make_occupancy_grid(int(gs[0]), int(gs[1]), float(gs[2]), float(gs[3])))
     pipe.grid_update_counter = int(z["counter0"])
     pipe.capture_zall = []
+    pipe.capture_coarse = []
     res = pipe.render_image(int(z["H"]), int(z["W"]), z["pose"], z["K"])
     ev, full = pipe.evaluated_samples()
     got = {k: v.cpu().numpy() for k, v in res.items()}
@@ -527,6 +580,8 @@ def test_lego_yaml_eval_frame_through_plugin(dev, prec):
                  "pose": torch.from_numpy(z["pose"])[None],
                  "intrinsics": torch.from_numpy(z["K"])[None]}
         rend.pipeline.capture_zall = []
+        rend.pipeline.capture_coarse = []
+    rend.pipeline.capture_coarse = []
         with torch.no_grad():
             out = rend.render(batch)
     finally:

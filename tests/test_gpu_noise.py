@@ -97,6 +97,37 @@ def test_noise_fine_pass_given_reference_depths(dev, name, prec):
     assert rel_err(out[1].cpu().numpy(), z["out_disp_map"].reshape(n), floor=1e-3) < 1e-4
 
 
+@pytest.mark.parametrize("name", NOISE)
+def test_noise_render_chunks_per_rank_equals_one_pass(dev, name):
+    """The multi-GPU interleaved path with density noise: each of two ranks
+    renders its own reference chunk (chunk c on rank c mod 2,
+    NerfPipeline.render_chunks, the frame's t_rand and noise read by rows; with
+    ESS + ERT the other rank's grid-updating chunk replayed) and the chunks put
+    back in pixel order equal the one-pass noisy render bit for bit, final grid
+    and counter included (VR:147-205, 310-314, 1098-1103)."""
+    z = load(name)
+    H, W = int(z["H"]), int(z["W"])
+    n = H * W
+    assert n > 2048   # two reference chunks
+    tr, nz = _t(z["t_rand"], dev), _noise(z, dev)
+    one_pipe = _pipe(dev, z, "f16x3")
+    one = {k: v.cpu().numpy() for k, v in
+           one_pipe.render_image(H, W, z["pose"], z["K"], t_rand=tr, noise=nz).items()}
+    parts, pipes = [], []
+    for r in range(2):
+        p = _pipe(dev, z, "f16x3")
+        parts.append({k: v.cpu().numpy() for k, v in
+                      p.render_chunks(H, W, z["pose"], z["K"], [r], t_rand=tr, noise=nz).items()})
+        pipes.append(p)
+    for k, v in one.items():
+        got = np.concatenate([parts[0][k], parts[1][k]], 0)
+        assert np.array_equal(got.reshape(-1), v.reshape(-1), equal_nan=True), k
+    for p in pipes:
+        assert p.grid_update_counter == one_pipe.grid_update_counter
+        if one_pipe.grid is not None:
+            assert torch.equal(p.grid, one_pipe.grid)
+
+
 def test_add_sigma_noise_kernel(dev):
     """nerf_add_sigma_noise: .w + noise as one float32 add, rgb untouched, in place too."""
     from nerfhip._lib import call, ptr, stream_of

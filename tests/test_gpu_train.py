@@ -408,6 +408,53 @@ def test_side_stream_weight_grads_equal_inline(dev, mode, monkeypatch):
     assert not train_mlp._SIDE_SCOPE[0]
 
 
+@pytest.mark.parametrize("reader", ["tensor_hook", "post_accumulate_hook", "create_graph"])
+def test_side_stream_join_waits_for_main_stream_readers(dev, reader, monkeypatch):
+    """Inside side_wgrad_scope the main stream may read a side-stream weight
+    gradient before the pass ends: a tensor hook and a post-accumulate-grad
+    hook run there, and with create_graph AccumulateGrad copies the gradient
+    there. The join then waits at once, so what each reader sees equals the
+    in-line schedule bit for bit (a read before the side stream finished
+    would show as a partial or stale gradient)."""
+    from nerfhip import train_mlp
+    from nerfhip.train import NerfTrainer
+    from nerfhip.train_mlp import prepack, side_wgrad_scope
+    z, _, ro, rd, _, _, gt = _setup(dev, "x3")
+    g = torch.Generator(device=dev).manual_seed(11)
+    n = ro.shape[0]
+    t_rand = torch.rand((n, 64), device=dev, generator=g)
+    u = torch.rand((n, 128), device=dev, generator=g)
+    runs = {}
+    for side in (False, True):
+        monkeypatch.setattr(train_mlp, "SIDE_WGRAD", side)
+        tr = NerfTrainer(dev, params_of(z), mlp="x3")
+        fine = dict(tr.fine.named_parameters())
+        seen = []
+        hooks = []
+        if reader == "tensor_hook":   # every fine weight: the hook clones on the main stream
+            for k in ("pts_linears.0.weight", "pts_linears.7.weight", "rgb_linear.weight"):
+                hooks.append(fine[k].register_hook(lambda gr: seen.append(gr.clone())))
+        elif reader == "post_accumulate_hook":
+            for k in ("pts_linears.3.weight", "views_linears.0.weight"):
+                hooks.append(fine[k].register_post_accumulate_grad_hook(
+                    lambda q: seen.append(q.grad.clone())))
+        tr.opt.zero_grad(set_to_none=True)
+        prepack([tr.coarse, tr.fine])
+        loss = tr.loss(tr.forward(ro, rd, t_rand, u), gt)["loss"]
+        with side_wgrad_scope([tr.fine]):
+            loss.backward(create_graph=reader == "create_graph")
+        torch.cuda.synchronize()
+        for h in hooks:
+            h.remove()
+        runs[side] = (seen, {k: q.grad.detach().clone() for k, q in fine.items()})
+    assert len(runs[True][0]) == len(runs[False][0])
+    for a, b in zip(runs[False][0], runs[True][0]):
+        assert torch.equal(a, b)
+    for k, a in runs[False][1].items():
+        assert torch.equal(a, runs[True][1][k]), k
+    assert not train_mlp._SIDE_SCOPE[0]
+
+
 def test_hip_adam_matches_torch_adam(dev):
     """HipAdam (clip_grad_value_ + Adam in one nerf_adam_step launch) against
     torch.optim.Adam (foreach=False) after torch's clip_grad_value_, 6 steps on

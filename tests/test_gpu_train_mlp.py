@@ -119,6 +119,47 @@ def test_tiny_sigma_gradient_keeps_its_split_range(dev, P, monkeypatch):
     assert max(errs.values()) < 1e-4, errs
 
 
+@pytest.mark.parametrize("shared", [True, False])
+@pytest.mark.parametrize("gain", [2.0 ** -10, 2.0 ** -14])
+def test_small_views_output_keeps_rgb_gradient_precision(dev, shared, gain, monkeypatch):
+    """The shared views-encoding / rgb weight-gradient tile multiplies
+    [d hv; d sigma; d rgb] by [view enc; HV]^T with ONE FP16 split range for B,
+    max(max |enc|, max |HV|). The views layer's output HV scaled down by
+    `gain` (its weight and bias x gain, the rgb head x 1/gain: the same network
+    in real arithmetic) sits far below the encoding's |.| <= 1 there; the split
+    keeps about 21 bits while max |HV| >= 2^-16 of the range (the low half stays
+    an FP16 normal). Every gradient, rgb_linear's included, within 1e-4 of
+    torch FP32 autograd of the reference module (network.py:49-74), with the
+    shared tile and with the two tiles of its own (NERF_TRAIN_ENC_RGB_TILE=0).
+    The fused backward also zeroes the rows between d sigma and d rgb that the
+    shared tile reads (rows 129..143 of its A operand: discarded products, but
+    never uninitialised memory)."""
+    from nerfhip import train_mlp
+    from nerfhip.train import freq_encode
+    from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
+    monkeypatch.setattr(train_mlp, "FUSED_FORWARD", True)
+    monkeypatch.setattr(train_mlp, "FUSED_BACKWARD", True)
+    monkeypatch.setattr(train_mlp, "ENC_RGB_TILE", shared)
+    m = _model(dev)
+    with torch.no_grad():
+        m.views_linears[0].weight.mul_(gain)
+        m.views_linears[0].bias.mul_(gain)
+        m.rgb_linear.weight.mul_(1.0 / gain)
+    P = 1024
+    pts, dirs = _inputs(dev, P)
+    d_raw = torch.randn((P, 4), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    d_raw[_relu_edge_samples(m, pts, dirs)] = 0.0
+    x = pts.clone().requires_grad_(True)
+    ref = m(torch.cat([freq_encode(x, 10), freq_encode(dirs, 4)], -1))
+    ref_grads = torch.autograd.grad(ref, [x] + mlp_params(m), d_raw)
+    y = pts.clone().requires_grad_(True)
+    out = NerfMLPFn.apply(y, dirs, *mlp_params(m))
+    got = torch.autograd.grad(out, [y] + mlp_params(m), d_raw)
+    errs = {name: _rel(a, b) for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads)}
+    assert errs["rgb_linear.weight"] < 1e-4 and errs["rgb_linear.bias"] < 1e-4, errs
+    assert max(errs.values()) < 1e-4, errs
+
+
 def test_x3_layer_kernel_matches_matmul(dev):
     """One nerf_x3_layer launch per supported shape: bias + ReLU + mask + rank-1."""
     from nerfhip.train_mlp import _layer, pack_x3_matrix
