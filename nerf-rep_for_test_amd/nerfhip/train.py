@@ -301,6 +301,7 @@ class NerfTrainer:
             self.opt = torch.optim.Adam(self.trained_parameters(), lr=lr, eps=1e-8,
                                         weight_decay=0.0, fused=self.device.type == "cuda")
         self._graphs = {}
+        self._flat_draws = {}
         self._one = {}
         self._warm = {}
         self.z_base = coarse_depth_table(near, far, self.N_samples, False).to(self.device)
@@ -372,6 +373,13 @@ class NerfTrainer:
         return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
 
     def _draws(self, n, t_rand, u):
+        """The step's draws: both from ONE torch.rand launch when neither is
+        given (t_rand the first n * N_samples values, u the rest: the same
+        numbers in the eager and the graph step, _step_graphed)."""
+        if t_rand is None and u is None:
+            S, NI = self.N_samples, self.N_importance
+            flat = torch.rand((n * (S + NI),), device=self.device)
+            return flat[:n * S].view(n, S), flat[n * S:].view(n, NI)
         if t_rand is None:
             t_rand = torch.rand((n, self.N_samples), device=self.device)
         if u is None:
@@ -386,8 +394,16 @@ class NerfTrainer:
             if self._warm.get(key, 0) < 2:
                 self._warm[key] = self._warm.get(key, 0) + 1
                 return self._step_eager(rays_o, rays_d, target, t_rand, u, group)
-            static = tuple(x.detach().clone().contiguous()
-                           for x in (rays_o, rays_d, target, t_rand, u))
+            static = [x.detach().clone().contiguous() for x in (rays_o, rays_d, target)]
+            # the draws: views of one flat buffer, so a replay draws them with one
+            # torch.rand launch (the numbers _draws makes in an eager step)
+            n, S = t_rand.shape
+            flat = torch.empty((n * (S + u.shape[1]),), device=self.device, dtype=torch.float32)
+            static += [flat[:n * S].view(n, S), flat[n * S:].view(n, u.shape[1])]
+            static[3].copy_(t_rand)
+            static[4].copy_(u)
+            static = tuple(static)
+            self._flat_draws[key] = flat
             graph = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
             with torch.cuda.graph(graph):
@@ -398,11 +414,18 @@ class NerfTrainer:
         else:
             given = (rays_o, rays_d, target, t_rand, u)
         graph, static, out = g
-        for i, (dst, src) in enumerate(zip(static, given)):
-            if src is None:   # the step's draw, straight into the graph's input (t_rand, then u)
-                torch.rand(dst.shape, device=dst.device, out=dst)
-            elif src is not dst:
-                dst.copy_(src)
+        if given[3] is None and given[4] is None:   # both draws with one launch (_draws)
+            flat = self._flat_draws[key]
+            torch.rand(flat.shape, device=flat.device, out=flat)
+        else:
+            for dst, src in zip(static[3:], given[3:]):
+                if src is None:   # the step's draw, straight into the graph's input
+                    torch.rand(dst.shape, device=dst.device, out=dst)
+        # the batch (and any given draw) into the static inputs: one multi-tensor copy
+        pairs = [(dst, src) for dst, src in zip(static, given)
+                 if src is not None and src is not dst]
+        if pairs:
+            torch._foreach_copy_([d for d, _ in pairs], [s for _, s in pairs])
         graph.replay()
         return out
 

@@ -450,6 +450,7 @@ def _launch_packs(nets):
 
 
 _NETS = {}
+_STATS = {}   # prepack's zeroed amax / dmax slots, one buffer per set of networks
 
 
 def _net_for(params, device):
@@ -484,10 +485,15 @@ def prepack(networks, side=False):
             ps.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(ps):
                 _launch_packs(nets)
-                for n in nets:
-                    if n.stats is None:
-                        n.stats = torch.empty(25, device=dev, dtype=torch.float32)
-                    n.stats.zero_()
+                # every network's amax / dmax slots in one buffer: one fill
+                key = tuple(id(n) for n in nets)
+                buf = _STATS.get(key)
+                if buf is None or buf.device != dev:
+                    buf = _STATS[key] = torch.empty(25 * len(nets), device=dev,
+                                                    dtype=torch.float32)
+                buf.zero_()
+                for i, n in enumerate(nets):
+                    n.stats = buf[25 * i:25 * (i + 1)]
                     n.stats_ready = True
             ev = torch.cuda.Event()
             ev.record(ps)

@@ -40,7 +40,9 @@ held to:
   MLP + composite (ERT: each chunk's decision restored, VR:1116) on exactly those
   rows must give the reference's maps within tolerance (max ratio <= 1), save
   for rays whose own ERT cut sits within 1e-4 of the threshold by the oracle's
-  transmittance (counted, at most 5 per frame).
+  transmittance AND moves under one of the reference's own exact
+  reparametrisations (tests/golden/rs_<frame>.npz for r2 / r3,
+  make_ert_sensitivity.py; counted, at most 5 per frame).
 
 r0 runs through NerfPipeline (the bench path); r1 through the drop-in plugin
 ``Renderer(net).render(batch)`` with the reference's perturb draws replayed
@@ -225,8 +227,15 @@ def _tail_given_reference_depths(name, prec, z, zh, tail_pix, zall_hip, coarse_h
     rep["tail_given_ref_depths_max_err"] = {k: float(v.max()) for k, v in e.items()}
     rep["tail_given_ref_depths_max_ratio_all"] = float(ratio.max())
     over = np.flatnonzero(ratio > 1.0)
-    flips = _ert_threshold_flips(z, T[over], zall[over], float(z["thr"])) if ert and len(over) \
+    near = _ert_threshold_flips(z, T[over], zall[over], float(z["thr"])) if ert and len(over) \
         else np.zeros(len(over), bool)
+    # an exemption must be backed by the reference itself: the ray's own cut
+    # moves under at least one of its exact reparametrisations
+    # (rs_<frame>.npz, make_ert_sensitivity.py: whole 2048-ray chunks)
+    moved = _reference_moves_cut(name, T[over]) if ert and len(over) else np.zeros(len(over), bool)
+    flips = near & moved
+    rep["tail_given_ref_depths_ert_near_threshold"] = int(near.sum())
+    rep["tail_given_ref_depths_ert_near_threshold_not_moved_by_reference"] = int((near & ~moved).sum())
     rep["tail_given_ref_depths_ert_threshold_flips"] = int(flips.sum())
     keep = np.ones(m, bool)
     keep[over[flips]] = False
@@ -277,6 +286,23 @@ def _tail_causal_chain(T, zc_ref, wc_ref, zall_hip, coarse_hip, zh, fine):
 
 
 ERT_FLIP_REL = 1e-4
+
+
+def _reference_moves_cut(name, pix):
+    """Per pixel: does the reference's own ERT cut (argmax of T < thr, VR:1108-1118)
+    of its fine call move under one of its exact reparametrisations
+    (tests/golden/rs_<name>.npz ``cut_var`` vs ``cut_ref``, make_ert_sensitivity.py)?
+    False where the pixel's chunk was not re-rendered."""
+    fs = _fs(name)
+    out = np.zeros(len(pix), bool)
+    if fs is None or "cut_ref" not in fs:
+        return out
+    P = fs["pixels"].astype(np.int64)
+    pos = np.minimum(np.searchsorted(P, pix), len(P) - 1)
+    have = P[pos] == pix
+    mv = (fs["cut_var"] != fs["cut_ref"][None, :]).any(0)
+    out[have] = mv[pos[have]]
+    return out
 
 
 def _ert_threshold_flips(z, pix, zall, thr):
