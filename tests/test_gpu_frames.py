@@ -607,7 +607,6 @@ def test_lego_yaml_eval_frame_through_plugin(dev, prec):
                  "intrinsics": torch.from_numpy(z["K"])[None]}
         rend.pipeline.capture_zall = []
         rend.pipeline.capture_coarse = []
-    rend.pipeline.capture_coarse = []
         with torch.no_grad():
             out = rend.render(batch)
     finally:
