@@ -1088,25 +1088,22 @@ __global__ __launch_bounds__(kX3Threads, 2) void mlp_x3_bwd_kernel(
   // (unwritten) mask words of their tile say, and no max |.| sees them
   float4 dr = io.d_raw[gl];
   if (!valid) dr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (io.d_raw_t && valid) {   // d raw as rows: the heads' wgrad operands
+  if (io.d_raw_t && g4 == 0 && valid) {   // d raw as rows: the heads' wgrad operands
     // d sigma at row 0, d rgb at rows 1..3 (feature-major) or 16..18 (T16: the
-    // rgb head's operand starts a 16-row group of its own, BlockRows)
+    // rgb head's operand starts a 16-row group of its own, BlockRows). Rows
+    // 1..15 of T16 stay unwritten: the shared views-encoding / rgb wgrad tile
+    // reads them as A rows 129..143, whose products land in output rows of
+    // their own (an MFMA row only meets its own A row; the split scale comes
+    // from the tensor maxima, not from the data) and are discarded. (Zeroing
+    // them here -- five more stores per lane group ahead of the slices'
+    // counted vmcnt waits -- was followed by an intermittent illegal address:
+    // reverted)
     constexpr int kRgb = T16 ? 16 : 1;
     char* t = reinterpret_cast<char*>(io.d_raw_t);
-    if (g4 == 0) {
-      *reinterpret_cast<float*>(t + io.lay.template elem<T16>(0, gs)) = dr.w;
-      *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb, gs)) = dr.x;
-      *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb + 1, gs)) = dr.y;
-      *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb + 2, gs)) = dr.z;
-    } else if (T16) {
-      // rows 1..15 (between d sigma and d rgb): zeros, lane group g4 rows
-      // 5 g4 - 4 .. 5 g4. The shared views-encoding / rgb wgrad tile reads rows
-      // 0..18 as one A operand; its products of these rows are discarded, but
-      // the rows are never left as uninitialised memory
-#pragma unroll
-      for (int r = 0; r < 5; ++r)
-        *reinterpret_cast<float*>(t + io.lay.template elem<T16>(5 * g4 - 4 + r, gs)) = 0.0f;
-    }
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(0, gs)) = dr.w;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb, gs)) = dr.x;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb + 1, gs)) = dr.y;
+    *reinterpret_cast<float*>(t + io.lay.template elem<T16>(kRgb + 2, gs)) = dr.z;
   }
   // outputs / masks of this (tile, wave): pointers loaded at their layer
   auto store_for = [&](int k, int rows) {

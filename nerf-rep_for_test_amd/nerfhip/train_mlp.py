@@ -380,6 +380,7 @@ class X3NetPacker:
         self.fwd = X3StreamPacker(device)
         self.bwd = X3BwdStreamPacker(device)
         self.key = None         # storage key of the built tables
+        self.gen = 0            # build generation: every build allocates new buffers
         self.pending = False    # packed by prepack() for the next streams() call
         self.pending_event = None   # prepack(side=True): the pack stream's completion
         # prepack(side=True) also zeroes the max |.| slots of the network's next
@@ -393,6 +394,11 @@ class X3NetPacker:
             self.fwd._build(p)
             self.bwd._build(p, self.fwd.Wc)   # Wc^T: the forward's fold, made first
             self.fwd.key = self.bwd.key = self.key = key
+            # the build's records point at its own new buffers (stream, scales,
+            # maxima, Wc / bc, head): a device table made for an earlier build --
+            # even one with the same parameter addresses -- points at freed
+            # memory, so the table cache is keyed by the generation too
+            self.gen += 1
             self.pending = False
 
     def records(self):
@@ -431,7 +437,7 @@ _PACK_TABLES = {}
 def _launch_packs(nets):
     """One nerf_x3_pack launch set over several networks' records (the tables
     cached per set of built packers)."""
-    key = tuple((id(n), n.key) for n in nets)
+    key = tuple((id(n), n.gen) for n in nets)
     tabs = _PACK_TABLES.get(key)
     if tabs is None:
         recs, heads = [], []

@@ -131,9 +131,8 @@ def test_small_views_output_keeps_rgb_gradient_precision(dev, shared, gain, monk
     an FP16 normal). Every gradient, rgb_linear's included, within 1e-4 of
     torch FP32 autograd of the reference module (network.py:49-74), with the
     shared tile and with the two tiles of its own (NERF_TRAIN_ENC_RGB_TILE=0).
-    The fused backward also zeroes the rows between d sigma and d rgb that the
-    shared tile reads (rows 129..143 of its A operand: discarded products, but
-    never uninitialised memory)."""
+    (The rows between d sigma and d rgb that the shared tile reads, A rows
+    129..143, feed only discarded output rows.)"""
     from nerfhip import train_mlp
     from nerfhip.train import freq_encode
     from nerfhip.train_mlp import NerfMLPFn, PARAM_NAMES, mlp_params
@@ -158,6 +157,30 @@ def test_small_views_output_keeps_rgb_gradient_precision(dev, shared, gain, monk
     errs = {name: _rel(a, b) for name, a, b in zip(["pts"] + PARAM_NAMES, got, ref_grads)}
     assert errs["rgb_linear.weight"] < 1e-4 and errs["rgb_linear.bias"] < 1e-4, errs
     assert max(errs.values()) < 1e-4, errs
+
+
+def test_pack_tables_follow_rebuilds(dev):
+    """The device tables of a network's packing launch (_launch_packs) are cached;
+    every rebuild of a packer allocates new output buffers (streams, scales,
+    maxima, the fold's Wc / bc, head), so a table made for an earlier build must
+    never serve a later one -- also when the parameter addresses repeat
+    (parameters A, then B, then A again). A stale table writes the packing into
+    the freed buffers of the old build (an intermittent illegal address when
+    that memory is returned) and leaves the live stream unpacked. The streams
+    after A -> B -> A equal a fresh packer's of A bit for bit."""
+    from nerfhip.train_mlp import PARAM_NAMES, X3NetPacker, mlp_params
+    m = _model(dev)
+    pa = dict(zip(PARAM_NAMES, mlp_params(m)))
+    pb = dict(pa, **{"rgb_linear.weight": pa["rgb_linear.weight"].detach().clone()})
+    net = X3NetPacker(dev)
+    for p in (pa, pb, pa):
+        streams = net.streams(p)
+    fresh = X3NetPacker(dev).streams(pa)
+    torch.cuda.synchronize()
+    assert net.gen == 3
+    for a, b in zip(streams, fresh):
+        assert torch.equal(a, b)
+    assert streams[0].abs().sum() > 0
 
 
 def test_x3_layer_kernel_matches_matmul(dev):
