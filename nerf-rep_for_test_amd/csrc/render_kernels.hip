@@ -407,9 +407,6 @@ __global__ __launch_bounds__(64 * ERT_WAVES) void composite_ert_kernel(
 // product order (double accumulation both: ~1e-16 relative). One thread per
 // ray; one atomic per wave for the list slots.
 // ---------------------------------------------------------------------------
-#ifndef NERF_ERT_BATCH
-#define NERF_ERT_BATCH 8   // 1: the sample-by-sample loop (timing A/B only)
-#endif
 __global__ __launch_bounds__(256) void ert_segment_kernel(
     const float4* __restrict__ raw, const float* __restrict__ z, int64_t z_stride,
     const float* __restrict__ rays_d, int64_t n, int S, int s0, int s1, int s2, float thr,
@@ -423,29 +420,10 @@ __global__ __launch_bounds__(256) void ert_segment_kernel(
     if (s1 > s0) {
       const float* zr = z + r * z_stride;
       const float nd = torch_norm3(rays_d[r * 3], rays_d[r * 3 + 1], rays_d[r * 3 + 2]);
-      // the segment's loads issued together (kErtBatch samples at a time), then
-      // the product in sample order: one memory round trip per batch, not one
-      // per sample (the product, and so T, is the sequential form's bit for bit)
-      constexpr int kErtBatch = NERF_ERT_BATCH;
-      for (int sb = s0; sb < s1; sb += kErtBatch) {
-        float w[kErtBatch], z0[kErtBatch], z1[kErtBatch];
-#pragma unroll
-        for (int k = 0; k < kErtBatch; ++k) {
-          const int s = sb + k;
-          const bool in = s < s1;
-          w[k] = in ? raw[r * S + s].w : 0.0f;
-          z0[k] = in ? zr[s] : 0.0f;
-          z1[k] = in && s < S - 1 ? zr[s + 1] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < kErtBatch; ++k) {
-          const int s = sb + k;
-          if (s < s1) {
-            const float dist = ((s < S - 1) ? (z1[k] - z0[k]) : 1e10f) * nd;
-            const float a = 1.0f - expf((-fmaxf(w[k], 0.0f)) * dist);
-            t = t * (double)(1.0f - a);
-          }
-        }
+      for (int s = s0; s < s1; ++s) {
+        const float dist = ((s < S - 1) ? (zr[s + 1] - zr[s]) : 1e10f) * nd;
+        const float a = 1.0f - expf((-fmaxf(raw[r * S + s].w, 0.0f)) * dist);
+        t = t * (double)(1.0f - a);
       }
       T[r] = t;
     }
