@@ -56,6 +56,7 @@ GT_PATH = os.path.join(REPO, "data", "lego", "test.npz")
 TRAIN_PATH = os.path.join(REPO, "data", "lego", "train.npz")
 
 
+COLL = ["RCCL"]             # the collective library named in "parallelism"
 POSE_STRIDE = [GT_STRIDE]   # --all-poses: 1 (every one of the 200 test poses)
 
 
@@ -149,6 +150,7 @@ def main():
     # one-GPU box, ranks sharing the device; the driver's runs use RCCL ("nccl"),
     # one rank per GPU.
     backend = os.environ.get("NERF_DIST_BACKEND", "nccl")
+    COLL[0] = "RCCL" if backend == "nccl" else backend
     err = launch_mismatch(args.gpus, world, backend, args.config)
     if err:
         print(f"bench.py: {err}", file=sys.stderr)
@@ -269,8 +271,8 @@ def main():
                    "H": H, "W": W, "N_samples": 64, "N_importance": 128,
                    "mlp_precision": args.precision,
                    "parallelism": (f"2048-ray chunks dealt round-robin x{world} (chunk c -> rank "
-                                   f"c mod {world}) + RCCL all-gather of pixels" if c4 else
-                                   f"row-band tiles x{world} + RCCL all-gather of pixels")},
+                                   f"c mod {world}) + {COLL[0]} all-gather of pixels" if c4 else
+                                   f"row-band tiles x{world} + {COLL[0]} all-gather of pixels")},
         "roofline": roof,
         "build_id": _lib.build_id(),
     }
@@ -323,7 +325,7 @@ def main():
                                       "0.1) self-updated by the reference's rule), perturb 0, "
                                       "eval, 1 frame per step (test poses cycled)",
                           "baseline_config": "configs[3]",
-                          "parallelism": f"2048-ray chunks round-robin x{world} + RCCL "
+                          "parallelism": f"2048-ray chunks round-robin x{world} + {COLL[0]} "
                                          f"all-gather"},
                "roofline": {k: roof4[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
                                                   "avg_launch_ms", "launches")},
@@ -354,7 +356,7 @@ def main():
                                       "(test poses cycled)",
                           "baseline_config": "configs[3] as run.py --type evaluate renders it "
                                              "(lego.yaml)",
-                          "parallelism": f"2048-ray chunks round-robin x{world} + RCCL "
+                          "parallelism": f"2048-ray chunks round-robin x{world} + {COLL[0]} "
                                          f"all-gather"},
                "roofline": {k: roofy[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
                                                   "avg_launch_ms", "launches")},
@@ -382,7 +384,7 @@ def main():
                                    "frame, one [n, 64] uniform draw), eval-mode fine u, 1 frame "
                                    "per step (test poses cycled)",
                        "baseline_config": "configs[1] as run.py --type evaluate renders it",
-                       "parallelism": f"row-band tiles x{world} + RCCL all-gather of pixels"},
+                       "parallelism": f"row-band tiles x{world} + {COLL[0]} all-gather of pixels"},
             "roofline": {k: roofp[k] for k in ("kernel", "achieved", "peak", "unit", "frac",
                                                "avg_launch_ms", "launches", "mlp_share_of_step")}}
     if world == 1 and args.config == "c2" and not args.no_c3:
@@ -684,7 +686,7 @@ def bench_train(args, world, rank, dev, params, data, barrier, steps=None, warmu
                                   (f"; chosen by a 5-step calibration (ms/step: eager "
                                    f"{calib['eager']:.2f}, graph {calib['graph']:.2f})"
                                    if calib else ""),
-                   "parallelism": f"data parallel x{world} (RCCL all-reduce)"},
+                   "parallelism": f"data parallel x{world} ({COLL[0]} all-reduce)"},
         "roofline": train_roofline(args.train_mlp, flop, step_s),
         "loss_last": float(losses["loss"].item()),
         "build_id": __import__("nerfhip._lib", fromlist=["build_id"]).build_id(),

@@ -68,13 +68,17 @@ def unpack_maps(full, H, W, keys):
     return out
 
 
-def _collective(world):
-    """The gather runs whenever a process group is up -- at world 1 too, so the
-    RCCL all-gather and the reassembly are exercised by a one-GPU run
-    (tests/test_gpu_nccl.py: backend "nccl" at world 1, bit-equal to the
-    one-pass frame); with no group (a plain one-process render) the tile is the
-    frame."""
-    return world > 1 or (dist.is_available() and dist.is_initialized())
+def _collective(world, group=None):
+    """The gather runs for world > 1, and at world 1 whenever a one-rank
+    process group is up, so the RCCL all-gather and the reassembly are
+    exercised by a one-GPU run (tests/test_gpu_nccl.py: backend "nccl" at
+    world 1, bit-equal to the one-pass frame). With no group (a plain
+    one-process render), or a world-1 render inside a larger job, the tile is
+    the frame."""
+    if world > 1:
+        return True
+    return (dist.is_available() and dist.is_initialized()
+            and dist.get_world_size(group) == 1)
 
 
 def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
@@ -88,7 +92,7 @@ def render_frame_sharded(render_band, H, W, rank, world, device, group=None,
     maps = render_band(p0, n) or {}
     keys = set(maps) if maps else set(MAP_ORDER)
     tile = pack_maps(maps, n, n_pad, device)
-    if not _collective(world):
+    if not _collective(world, group):
         full = tile
     else:
         full = torch.empty((world * n_pad, 12), device=device, dtype=torch.float32)
@@ -138,7 +142,7 @@ def render_frame_interleaved(render_chunks, H, W, rank, world, device, group=Non
     maps = render_chunks(mine) or {}
     keys = set(maps) if maps else set(MAP_ORDER)
     tile = pack_maps(maps, n, n_pad, device)
-    if not _collective(world):
+    if not _collective(world, group):
         full = tile[:H * W]
     else:
         full = torch.empty((world * n_pad, 12), device=device, dtype=torch.float32)
