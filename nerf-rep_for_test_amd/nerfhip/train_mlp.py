@@ -1198,29 +1198,47 @@ class NerfMLPFn(torch.autograd.Function):
             else None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream(dev))
+        # with a side stream, this node's own input gradient is enqueued first: a
+        # short launch that would otherwise queue behind the weight gradients'
+        # workgroups (they fill every CU's LDS) and run only as they retire,
+        # holding back the coarse network's backward that waits for it (round 6,
+        # C3 graph step 2.757 / 2.735 ms vs 2.782 / 2.761 enqueued after:
+        # profiles/r6_t16_sample_major/ab.log)
+        d_pts = NerfMLPFn._input_grad(d_enc, E, pts, rays_S, P, dev) \
+            if side is not None and DZ_FIRST else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             NerfMLPFn._weight_grads(wb, post, grads, heads_merged, v_h7, p, dev)
         if side is not None:
             _join_side(side, wb, grads, (amax, dmax), params, dev)
-        d_pts = None
-        if d_enc is not None:   # (layer 5's, layer 0's) encoding rows, summed in the kernel
-            def lay(t):   # (row stride, T16 block stride) of an operand
-                return (BLOCK, t.block_stride) if isinstance(t, BlockRows) else (t.stride(0), 0)
-            assert lay(d_enc[0]) == lay(d_enc[1])
-            (ldd, bsd), (lde, bse) = lay(d_enc[0]), lay(E)
-            if rays_S:          # pts = the rays' o + d z: straight on to d z
-                d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
-                     ptr(E), lde, bse, ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
-                     _lib.stream_of(dev))
-            else:
-                d_pts = torch.empty((P, 3), device=dev, dtype=f32)
-                call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
-                     ptr(E), lde, bse, ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
-                     _lib.stream_of(dev))
+        if d_pts is None:
+            d_pts = NerfMLPFn._input_grad(d_enc, E, pts, rays_S, P, dev)
         if rays_S:
             return (None, None, d_pts, *[grads[n] for n in PARAM_NAMES])
         return (d_pts, None, *[grads[n] for n in PARAM_NAMES])
+
+    @staticmethod
+    def _input_grad(d_enc, E, pts, rays_S, P, dev):
+        """d z [P / S, S] (ray form) or d pts [P, 3] from the encoding rows' gradient
+        (layer 5's and layer 0's, summed in the kernel); None without one."""
+        if d_enc is None:
+            return None
+        f32 = torch.float32
+
+        def lay(t):   # (row stride, T16 block stride) of an operand
+            return (BLOCK, t.block_stride) if isinstance(t, BlockRows) else (t.stride(0), 0)
+        assert lay(d_enc[0]) == lay(d_enc[1])
+        (ldd, bsd), (lde, bse) = lay(d_enc[0]), lay(E)
+        if rays_S:          # pts = the rays' o + d z: straight on to d z
+            d_pts = torch.empty((P // rays_S, rays_S), device=dev, dtype=f32)
+            call("nerf_freq_encode_fm_backward_dz", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                 ptr(E), lde, bse, ptr(pts), rays_S, P, XYZ_FREQS, ptr(d_pts),
+                 _lib.stream_of(dev))
+        else:
+            d_pts = torch.empty((P, 3), device=dev, dtype=f32)
+            call("nerf_freq_encode_fm_backward_sum", ptr(d_enc[0]), ptr(d_enc[1]), ldd, bsd,
+                 ptr(E), lde, bse, ptr(pts), 3, P, XYZ_FREQS, ptr(d_pts),
+                 _lib.stream_of(dev))
+        return d_pts
 
     @staticmethod
     def _weight_grads(wb, post, grads, heads_merged, v_h7, p, dev):
@@ -1278,6 +1296,9 @@ class NerfMLPFn(torch.autograd.Function):
 ENC_RGB_TILE = _os.environ.get("NERF_TRAIN_ENC_RGB_TILE", "1") != "0"
 # NERF_TRAIN_SIDE_WGRAD=0: the weight gradients on the main stream, in line
 SIDE_WGRAD = _os.environ.get("NERF_TRAIN_SIDE_WGRAD", "1") != "0"
+# NERF_TRAIN_DZ_FIRST=0: with side-stream weight gradients, enqueue the node's
+# input gradient after them (the A/B of the order)
+DZ_FIRST = _os.environ.get("NERF_TRAIN_DZ_FIRST", "1") != "0"
 _SIDE = {}
 _SIDE_SCOPE = [frozenset()]   # a plain global: the autograd engine runs backward on its own thread
 
