@@ -143,3 +143,42 @@ def test_train_gradient_allreduce_mean():
         a, b = got[rank]
         assert (a == 1.5).all()
         assert (b == torch.arange(5).numpy() * 1.5).all()
+
+
+def _local_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        H, W = 7, 9
+        local = nd.render_frame_sharded(lambda p0, n: fake_render(p0, n), H, W, 0, 1,
+                                        torch.device("cpu"))
+        inter = nd.render_frame_interleaved(lambda cs: fake_render_chunks(cs, H * W), H, W, 0, 1,
+                                            torch.device("cpu"))
+        q.put((rank, nd._collective(1), nd._collective(world),
+               {k: v.numpy().copy() for k, v in local.items()},
+               {k: v.numpy().copy() for k, v in inter.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world_one_render_inside_larger_job_stays_local():
+    """A world-1 frame rendered by one rank of a 2-rank job (its own full frame,
+    e.g. an evaluation on every rank) takes no collective: the tile is the
+    frame, equal to the single-process render; world 2 does gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = fake_render(0, 7 * 9)
+    for rank in (0, 1):
+        c1, c2, local, inter = got[rank]
+        assert c1 is False and c2 is True
+        for k, v in ref.items():
+            want = v.numpy().reshape(local[k].shape)
+            assert (local[k] == want).all() and (inter[k] == want).all(), k
