@@ -73,3 +73,43 @@ def test_kilonerf_module_exports_reference_op_names():
     assert len(ops) == 22
     for op in ops:
         assert callable(getattr(kilonerf_cuda, op)), op
+
+
+_PROBE = r'''
+import ctypes as C, json, sys
+sys.path.insert(0, sys.argv[1])
+from nerfhip import _lib
+L = _lib.lib()
+out = {}
+for name, (restype, argtypes) in sorted(_lib.SIGNATURES.items()):
+    ptrs = [a in (C.c_void_p, C.c_char_p) or (isinstance(a, type) and issubclass(a, C._Pointer))
+            for a in argtypes]
+    if restype is not C.c_int or not any(ptrs):
+        continue
+    args = [None if p else (1.0 if a in (C.c_float, C.c_double) else
+                            (False if a is C.c_bool else 1))
+            for p, a in zip(ptrs, argtypes)]
+    rc = getattr(L, name)(*args)
+    out[name] = (rc, L.nerf_last_error().decode())
+print(json.dumps(out))
+'''
+
+
+def test_every_entry_rejects_null_pointers(lib_path):
+    """Every C-ABI entry point that takes a pointer, called with null pointers
+    and unit sizes, returns an error code with a message naming it -- before any
+    HIP call, so it runs here without a GPU -- and never crashes or exits the
+    process (the reference's gpuErrchk exits, utils.cu:10-19). Run in a child
+    process so a crash would fail this test rather than the session."""
+    import json
+    import sys
+    pkg = os.path.join(REPO, "nerf-rep_for_test_amd")
+    r = subprocess.run([sys.executable, "-c", _PROBE, pkg], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(got) >= 50, sorted(got)
+    for name, (rc, msg) in got.items():
+        assert rc != 0, name
+        stem = name.replace("_ex", "").replace("_rays", "").replace("_sum", "")
+        assert msg.split(":")[0] in name or stem.startswith(msg.split(":")[0]), (name, msg)
